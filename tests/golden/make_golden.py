@@ -1,0 +1,308 @@
+"""Generate the golden parity fixtures from the REFERENCE implementation (build container only).
+
+    python tests/golden/make_golden.py          # writes tests/golden/*.npz
+
+Runs the reference modules from /root/reference (imported via ``ref_import.py``) on CPU under
+``torch.autocast("cpu", bfloat16)``, which with the amp shim reproduces the CUDA autocast precision
+flow of the training scripts (`train_prfl.py:686,723,762`).  Weights and inputs come from
+``seeded.py``.  The fixtures hold inputs and outputs only (data); the GPU box regenerates the
+same weights from ``seeded.py``.  Each case cites the reference lines it exercises.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import seeded  # noqa: E402
+from ref_import import import_reference  # noqa: E402
+
+torch.set_num_threads(8)
+M, NET, UNIPC, FM, DU = import_reference()
+AC = dict(device_type="cpu", dtype=torch.bfloat16)
+
+TOY = dict(dim=256, ffn_dim=512, freq_dim=256, text_dim=64, num_heads=2, num_layers=2,
+           out_dim=16, text_len=512)
+TOY_LATENT = (16, 3, 10, 14)     # -> grid (3,5,7), L=105 (not a multiple of any tile)
+
+
+def np32(t):
+    return t.detach().float().cpu().numpy()
+
+
+def load_seeded(module, seed=seeded.BASE_SEED, prefix=""):
+    shapes = [(k, tuple(v.shape)) for k, v in module.state_dict().items()]
+    sd = seeded.make_state_dict([(prefix + k, s) for k, s in shapes], seed)
+    sd = {k[len(prefix):]: torch.from_numpy(v) for k, v in sd.items()}
+    module.load_state_dict(sd)
+    return module
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: (v if isinstance(v, np.ndarray) else np.asarray(v))
+                                 for k, v in arrs.items()})
+    print("wrote", path, f"{os.path.getsize(path)/1e6:.2f} MB")
+
+
+def grads_of(module, keep_full=True, head=256, full_max=70000):
+    """Full grads for small params; for large ones: norm, first `head` values and a projection
+    onto a seeded random vector (`gproj`), which pins every element at O(1/sqrt(n)) weight."""
+    out = {}
+    for n, p in module.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().float().flatten()
+        if keep_full and g.numel() <= full_max:
+            out["grad/" + n] = g.numpy()
+        else:
+            r = torch.from_numpy(seeded.randn("proj:" + n, (g.numel(),)))
+            out["gnorm/" + n] = np.float64(g.double().norm().item())
+            out["ghead/" + n] = g[:head].numpy()
+            out["gproj/" + n] = np.float64((g.double() * r.double()).sum().item())
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+def case_ops():
+    """rope_apply (`model.py:61-103`), WanRMSNorm (`:106-122`), WanLayerNorm (`:125-135`)."""
+    d = 128
+    freqs = torch.cat([M.rope_params(1024, d - 4 * (d // 6)), M.rope_params(1024, 2 * (d // 6)),
+                       M.rope_params(1024, 2 * (d // 6))], dim=1)
+    x = torch.from_numpy(seeded.randn("rope.x", (1, 112, 2, d)))
+    grid = torch.tensor([[3, 5, 7]])
+    rope = M.rope_apply(x, grid, freqs)                       # 105 rotated + 7 pass-through rows
+    rms = load_seeded(M.WanRMSNorm(256, eps=1e-6), prefix="rms.norm_q.")
+    xr = torch.from_numpy(seeded.randn("rms.x", (1, 40, 256), 3.0)).to(torch.bfloat16)
+    rms_out = rms(xr)                                          # bf16 * fp32 weight -> fp32
+    ln = M.WanLayerNorm(256, 1e-6)
+    ln_aff = load_seeded(M.WanLayerNorm(256, 1e-6, elementwise_affine=True), prefix="ln.norm3.")
+    xl = torch.from_numpy(seeded.randn("ln.x", (1, 40, 256), 2.0)) + 0.5
+    save("ops", freqs_real=np.ascontiguousarray(torch.view_as_real(freqs).numpy()),
+         rope_x=np32(x), rope_grid=grid.numpy(), rope_out=np32(rope),
+         rms_x=np32(xr), rms_w=np32(rms.weight), rms_out=np32(rms_out),
+         ln_x=np32(xl), ln_out=np32(ln(xl)), ln_out_bf16in=np32(ln(xl.to(torch.bfloat16))),
+         ln_aff_w=np32(ln_aff.weight), ln_aff_b=np32(ln_aff.bias), ln_aff_out=np32(ln_aff(xl)))
+
+
+def _toy_model(model_type):
+    torch.manual_seed(0)
+    in_dim = 16 if model_type == "t2v" else 36
+    m = M.WanModel(model_type=model_type, in_dim=in_dim, **TOY)
+    m.__class__.enable_teacache = False
+    return load_seeded(m, prefix="toy.")
+
+
+def case_toy_model(model_type):
+    """WanModel.forward/backward end to end (`model.py:534-705`), T2V and I2V."""
+    m = _toy_model(model_type)
+    x = torch.from_numpy(seeded.randn(model_type + ".x", TOY_LATENT)).requires_grad_(True)
+    ctx = torch.from_numpy(seeded.randn(model_type + ".ctx", (20, TOY["text_dim"])))
+    t = torch.tensor([700])
+    L = 3 * 5 * 7
+    kw = {}
+    extra = {}
+    if model_type == "i2v":
+        y = torch.from_numpy(seeded.randn("i2v.y", (20,) + TOY_LATENT[1:]))
+        clip = torch.from_numpy(seeded.randn("i2v.clip", (1, 257, 1280)))
+        kw = dict(y=[y], clip_fea=clip)
+        extra = dict(y=np32(y), clip=np32(clip))
+    with torch.autocast(**AC):
+        out = m(x=[x], t=t, context=[ctx], seq_len=L, **kw)[0]
+    w = torch.from_numpy(seeded.randn(model_type + ".w", tuple(out.shape)))
+    (out * w).sum().backward()
+    # LRM feature tap (`model.py:656-670`, `train_prfl.py:762-767`)
+    m.zero_grad()
+    with torch.autocast(**AC):
+        feats = m(x=[x.detach()], t=t, context=[ctx], seq_len=L, output_features=True,
+                  selected_layers=[1], **kw)
+    save("toy_" + model_type, x=np32(x), ctx=np32(ctx), t=t.numpy(), out=np32(out),
+         upstream=np32(w), dx=np32(x.grad), feat1=np32(feats[0]), **extra,
+         **{k: v for k, v in _saved_grads.items()})
+
+
+_saved_grads = {}
+
+
+def case_toy_model_with_grads(model_type):
+    m = _toy_model(model_type)
+    global _saved_grads
+    x = torch.from_numpy(seeded.randn(model_type + ".x", TOY_LATENT)).requires_grad_(True)
+    ctx = torch.from_numpy(seeded.randn(model_type + ".ctx", (20, TOY["text_dim"])))
+    t = torch.tensor([700])
+    kw = {}
+    if model_type == "i2v":
+        kw = dict(y=[torch.from_numpy(seeded.randn("i2v.y", (20,) + TOY_LATENT[1:]))],
+                  clip_fea=torch.from_numpy(seeded.randn("i2v.clip", (1, 257, 1280))))
+    with torch.autocast(**AC):
+        out = m(x=[x], t=t, context=[ctx], seq_len=105, **kw)[0]
+    w = torch.from_numpy(seeded.randn(model_type + ".w", tuple(out.shape)))
+    (out * w).sum().backward()
+    _saved_grads = grads_of(m)
+
+
+def _real_block(kind):
+    blk = M.WanAttentionBlock(kind, 5120, 13824, 40, (-1, -1), True, True, 1e-6)
+    return load_seeded(blk, prefix="blocks.0.")
+
+
+def case_real_block(kind):
+    """One 14B WanAttentionBlock fwd/bwd at real width (C=5120, 40 heads, F=13824), L=48."""
+    tag = "t2v" if kind.startswith("t2v") else "i2v"
+    blk = _real_block(kind)
+    d = 128
+    freqs = torch.cat([M.rope_params(1024, d - 4 * (d // 6)), M.rope_params(1024, 2 * (d // 6)),
+                       M.rope_params(1024, 2 * (d // 6))], dim=1)
+    L, Lc = 48, (512 if tag == "t2v" else 769)
+    x = torch.from_numpy(seeded.randn("blk.x", (1, L, 5120))).requires_grad_(True)
+    e = torch.from_numpy(seeded.randn("blk.e", (1, 6, 5120), 0.1)).requires_grad_(True)
+    ctx = torch.from_numpy(seeded.randn("blk.ctx" + tag, (1, Lc, 5120))).to(torch.bfloat16)
+    ctx.requires_grad_(True)
+    grid = torch.tensor([[2, 4, 6]])
+    with torch.autocast(**AC):
+        out = blk(x, e, torch.tensor([L]), grid, freqs, ctx, None)
+    up = torch.from_numpy(seeded.randn("blk.up" + tag, (1, L, 5120)))
+    (out * up).sum().backward()
+    # inputs are regenerated from seeded.py on the GPU box (names above); dctx is summarised
+    g = ctx.grad.detach().float().flatten()
+    r = torch.from_numpy(seeded.randn("proj:dctx", (g.numel(),)))
+    save("real_block_" + tag, grid=grid.numpy(), out=np32(out), dx=np32(x.grad), de=np32(e.grad),
+         dctx_head=np32(ctx.grad[0, :8]), dctx_norm=np.float64(g.double().norm().item()),
+         dctx_proj=np.float64((g.double() * r.double()).sum().item()),
+         **grads_of(blk, keep_full=False))
+
+
+def case_reward_head():
+    """QueryAttention + MLP + sigmoid + PRFL hinge (`network.py:8-152`, `train_prfl.py:780-798`)."""
+    qa = NET.QueryAttention(feature_dim=5120, num_queries=1, num_heads=8, dropout=0.,
+                            return_type="query")
+    load_seeded(qa, prefix="qa.")
+    mlp = load_seeded(NET.MLP(5120), prefix="mlp.")
+    feats = torch.from_numpy(seeded.randn("qa.feat", (1, 1, 48, 5120), 1.0)).requires_grad_(True)
+    with torch.autocast(**AC):
+        pooled = qa(feats)                                   # 4-D path (`network.py:65-69`)
+        r = NET.forward_mlp(mlp, pooled)
+        loss = 0.1 * torch.relu(-r.squeeze() + 2).mean()
+    loss.backward()
+    save("reward_head", feat=np32(feats), pooled=np32(pooled), reward=np32(r), loss=np32(loss),
+         dfeat=np32(feats.grad), **{k: v for k, v in grads_of(qa).items()}, **grads_of(mlp))
+
+
+def case_schedulers():
+    """FlowUniPCMultistepScheduler (`fm_solvers_unipc.py`) and FlowMatchDiscreteScheduler."""
+    sch = UNIPC.FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                            use_dynamic_shifting=False)
+    sch.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
+    ts = sch.timesteps.clone()
+    sig = sch.sigmas.clone()
+    lat = torch.from_numpy(seeded.randn("unipc.lat", (1, 16, 3, 10, 14))).to(torch.bfloat16)
+    traj, outs = [], []
+    for i in range(6):
+        mo = torch.from_numpy(seeded.randn(f"unipc.mo{i}", (1, 16, 3, 10, 14)))
+        outs.append(np32(mo))
+        lat = sch.step(mo, ts[i], lat, return_dict=False)[0]
+        traj.append(np32(lat))
+    # differentiable step (the reward gradient path, `train_prfl.py:733-735`)
+    mo = torch.from_numpy(seeded.randn("unipc.mo6", (1, 16, 3, 10, 14))).requires_grad_(True)
+    prev = sch.step(mo, ts[6], lat, return_dict=False)[0]
+    w = torch.from_numpy(seeded.randn("unipc.w", (1, 16, 3, 10, 14)))
+    (prev.float() * w).sum().backward()
+    fm = FM.FlowMatchDiscreteScheduler(shift=5.0)
+    fm.set_timesteps(1000, dtype=torch.int64)
+    torch.manual_seed(7)
+    t_s, s_s = fm.get_train_timestep_and_sigma(weighting_scheme="uniform", batch_size=1,
+                                               n_dim=5)
+    save("schedulers", unipc_timesteps=ts.numpy(), unipc_sigmas=sig.numpy(),
+         unipc_lat0=np32(torch.from_numpy(seeded.randn("unipc.lat", (1, 16, 3, 10, 14)))
+                         .to(torch.bfloat16)),
+         unipc_model_outputs=np.stack(outs), unipc_traj=np.stack(traj), unipc_mo6=np32(mo),
+         unipc_prev6=np32(prev), unipc_w=np32(w), unipc_dmo6=np32(mo.grad),
+         fm_sigmas=fm.sigmas.numpy(), fm_timesteps=fm.timesteps.numpy(),
+         fm_sample_t=t_s.numpy(), fm_sample_sigma=np32(s_s))
+
+
+def case_toy_prfl():
+    """Toy PRFL reward step + SFT step, restating `train_prfl.py:585-835` and `:900-977`."""
+    gen = _toy_model("t2v")
+    lrm = _toy_model("t2v")
+    lrm.blocks = torch.nn.ModuleList([lrm.blocks[0]])      # trainable_blocks [0] (`:241-254`)
+    del lrm.head
+    lrm.head = None
+    for p in lrm.parameters():
+        p.requires_grad_(False)
+    qa = load_seeded(NET.QueryAttention(256, 1, 8, 0., return_type="query"), prefix="tqa.")
+    mlp = load_seeded(NET.MLP(256), prefix="tmlp.")
+    for p in list(qa.parameters()) + list(mlp.parameters()):
+        p.requires_grad_(False)
+    sch = UNIPC.FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                            use_dynamic_shifting=False)
+    sch.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
+    ts = sch.timesteps
+    ctx = torch.from_numpy(seeded.randn("prfl.ctx", (1, 20, TOY["text_dim"]))).to(torch.bfloat16)
+    latent = torch.from_numpy(seeded.randn("prfl.noise", (1,) + TOY_LATENT)).to(torch.bfloat16)
+    mid = 3
+    L = 105
+    with torch.no_grad():
+        for i in range(mid):
+            with torch.autocast(**AC):
+                npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[i]]),
+                                          context=DU.batch2list(ctx), seq_len=L))
+                latent = sch.step(npred, ts[i], latent, return_dict=False)[0]
+    roll = latent.clone()
+    with torch.autocast(**AC):
+        npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[mid]]),
+                                  context=DU.batch2list(ctx), seq_len=L))
+    latent = sch.step(npred, ts[mid], latent, return_dict=False)[0]
+    with torch.autocast(**AC):
+        feats = DU.list2batch(lrm(x=DU.batch2list(latent), t=torch.tensor([ts[mid + 1]]),
+                                  context=DU.batch2list(ctx), seq_len=L, output_features=True,
+                                  selected_layers=[1]))
+        r = NET.forward_mlp(mlp, qa(feats))
+        loss = 0.1 * torch.relu(-r.squeeze() + 2).mean()
+    loss = loss / 5.0
+    loss.backward()
+    g_reward = grads_of(gen)
+    # SFT flow-matching step (`:900-971`), fixed draw
+    gen.zero_grad()
+    fm = FM.FlowMatchDiscreteScheduler(shift=5.0)
+    fm.set_timesteps(1000, dtype=torch.int64)
+    x0 = torch.from_numpy(seeded.randn("sft.x0", (1,) + TOY_LATENT)).to(torch.bfloat16)
+    noise = torch.from_numpy(seeded.randn("sft.noise", (1,) + TOY_LATENT)).to(torch.bfloat16)
+    idx = 613
+    timestep = fm.timesteps[[idx]]
+    sigma = fm.sigmas[[idx]].float().view(1, 1, 1, 1, 1)
+    noisy = fm.add_noise(x0, noise, sigma)
+    with torch.autocast(**AC):
+        pred = DU.list2batch(gen(x=DU.batch2list(noisy), t=timestep, context=DU.batch2list(ctx),
+                                 seq_len=L))
+    target = fm.get_train_target(x0, noise)
+    sft_loss = torch.mean((pred.float() - target.float()) ** 2) / 5.0
+    sft_loss.backward()
+    g_sft = {"sft:" + k: v for k, v in grads_of(gen).items()}
+    save("toy_prfl", ctx=np32(ctx), noise=np32(torch.from_numpy(
+        seeded.randn("prfl.noise", (1,) + TOY_LATENT)).to(torch.bfloat16)), mid=np.int64(mid),
+        rollout=np32(roll), npred=np32(npred), stepped=np32(latent), feat=np32(feats),
+        reward=np32(r), loss=np32(loss), x0=np32(x0), sft_noise=np32(noise), sft_idx=np.int64(idx),
+        sft_timestep=fm.timesteps[[idx]].numpy(), sft_sigma=np32(sigma), sft_pred=np32(pred),
+        sft_loss=np32(sft_loss), **g_reward, **g_sft)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl"]
+    if "ops" in which:
+        case_ops()
+    if "toy" in which:
+        for mt in ("t2v", "i2v"):
+            case_toy_model_with_grads(mt)
+            case_toy_model(mt)
+    if "real" in which:
+        case_real_block("t2v_cross_attn")
+        case_real_block("i2v_cross_attn")
+    if "head" in which:
+        case_reward_head()
+    if "sched" in which:
+        case_schedulers()
+    if "prfl" in which:
+        case_toy_prfl()
