@@ -1,0 +1,504 @@
+// Flash attention forward / backward for the Wan DiT (head_dim 128, non-causal, key-length mask).
+//
+// Replaces the flash_attn varlen call at `wan/modules/attention.py:96-127` (reached from
+// `model.py:188` self-attn, `:221,:262,:264` cross-attn).  Tokens stay in the reference layout
+// [B, L, H*128] (row stride ld), so q/k/v come straight out of the fused QKV GEMM with no
+// permute.  Softmax statistics are kept in the log2 domain: LSE2 = max + log2(sum).
+//
+// Forward: one workgroup = 4 waves x 32 query rows; K/V tiles of 64 keys are register-staged
+// into a double-buffered LDS ring.  S^T = K.Q^T is computed with the key on the MFMA row so that
+// every query row lives on one lane column: the softmax statistics are per-lane scalars and the
+// S^T accumulator, packed to bf16, is directly the B operand of O^T = V^T.P^T (the 16x16x32
+// k-slot order is permuted consistently on both operands; V^T fragments come from
+// ds_read_b64_tr_b16 on the row-major V tile).
+//
+// Backward (FA2 recomputation, no atomics): delta = rowsum(dO*O); a dK/dV kernel owns 128 keys
+// per workgroup (32 per wave, accumulators resident) and sweeps all query tiles; a dQ kernel owns
+// 128 queries and sweeps all key tiles.  Both reuse the same lane mappings as the forward.
+#include "common.h"
+
+namespace {
+constexpr int HD = 128;
+constexpr float NEG_INF = -__builtin_huge_valf();
+
+struct AttnArgs {
+  const bf16* Q; int64_t ldq, bq;
+  const bf16* K; int64_t ldk, bk;
+  const bf16* V; int64_t ldv, bv;
+  bf16* O; int64_t ldo, bo;
+  float* LSE;            // [B][H][Lq], log2 domain
+  int Lq, Lk, H, k_len;
+  float sl2;             // softmax_scale * log2(e)
+};
+
+struct AttnBwdArgs {
+  const bf16* Q; int64_t ldq, bq;
+  const bf16* K; int64_t ldk, bk;
+  const bf16* V; int64_t ldv, bv;
+  const bf16* dO; int64_t lddo, bdo;
+  const float* LSE;      // [B][H][Lq] log2 domain
+  const float* Delta;    // [B][H][Lq]
+  bf16* dQ; int64_t lddq, bdq;
+  bf16* dK; int64_t lddk, bdk;
+  bf16* dV; int64_t lddv, bdv;
+  int Lq, Lk, H, k_len;
+  float sl2, scale;
+};
+
+// LDS images (256-B rows of 128 bf16):
+//  swz16: chunk ^ (row & 15)            -> conflict-free ds_read_b128 row reads
+//  swzT : byte ^ ((row & 7) << 5)       -> conflict-free ds_read_b64_tr_b16 reads
+//  swzB : chunk ^ (((row&3)<<2)|((row>>2)&3)) -> one image for both kinds of read
+__device__ __forceinline__ int off16(int row, int ch) { return row * 256 + ((ch ^ (row & 15)) << 4); }
+__device__ __forceinline__ int offT(int row, int byte) { return row * 256 + (byte ^ ((row & 7) << 5)); }
+__device__ __forceinline__ int offB(int row, int byte) {
+  return row * 256 + (byte ^ (((((row & 3) << 2) | ((row >> 2) & 3))) << 4));
+}
+
+// 16x16x32 B/A fragment of a row-major tile read with the hardware transpose.
+// Returns X^T fragment: lane (g, l16) gets rows {r0 + 4g + q, r0 + 16 + 4g + q}, column c0 + l16.
+template <int IMG>
+__device__ __forceinline__ bf16x8 tr_frag(const char* t, int r0, int c0, int lane) {
+  const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+  const int ra = r0 + 4 * g + q, rb = ra + 16;
+  const int byte = (c0 + 4 * p) * 2;
+  const int oa = IMG == 0 ? offT(ra, byte) : offB(ra, byte);
+  const int ob = IMG == 0 ? offT(rb, byte) : offB(rb, byte);
+  return cat8(lds_read_tr(t + oa), lds_read_tr(t + ob));
+}
+
+// row fragment: lane (g, l16) gets row r0 + l16, elements 32*ds + 8g .. +7
+template <int IMG>
+__device__ __forceinline__ bf16x8 row_frag(const char* t, int r0, int ds, int lane) {
+  const int row = r0 + (lane & 15), ch = ds * 4 + (lane >> 4);
+  const int o = IMG == 0 ? off16(row, ch) : offB(row, ch * 16);
+  return *(const bf16x8*)(t + o);
+}
+
+__device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
+  return (bf16x8){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]),
+                  f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+}
+
+// ============================================================================ forward ====
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int qr = min(q0 + w * 32 + sub * 16 + l16, a.Lq - 1);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) qf[sub][ds] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ds * 32 + g * 8);
+  }
+  f32x4 o[2][8];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {NEG_INF, NEG_INF}, l[2] = {0.f, 0.f};
+
+  const int nkv = (a.k_len + 63) / 64;
+  u32x4 rk[4], rv[4];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      const int key = min(t * 64 + row, a.Lk - 1);
+      rk[i] = *(const u32x4*)(Kb + (int64_t)key * a.ldk + ch * 8);
+      rv[i] = *(const u32x4*)(Vb + (int64_t)key * a.ldv + ch * 8);
+    }
+  };
+  auto sstore = [&](int st) {
+    char* Ks = smem + st * 32768;
+    char* Vs = Ks + 16384;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      *(u32x4*)(Ks + off16(row, ch)) = rk[i];
+      *(u32x4*)(Vs + offT(row, ch << 4)) = rv[i];
+    }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  for (int t = 0; t < nkv; ++t) {
+    const char* Ks = smem + (t & 1) * 32768;
+    const char* Vs = Ks + 16384;
+    if (t + 1 < nkv) gload(t + 1);
+    f32x4 s[2][4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) s[sub][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x8 kf = row_frag<0>(Ks, kt * 16, ds, lane);
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) s[sub][kt] = mfma16(kf, qf[sub][ds], s[sub][kt]);
+      }
+    const int kbase = t * 64;
+    if (kbase + 64 > a.k_len) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kbase + kt * 16 + 4 * g + r >= a.k_len) {
+            s[0][kt][r] = NEG_INF;
+            s[1][kt][r] = NEG_INF;
+          }
+    }
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      float mx = NEG_INF;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[sub][kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m[sub], mx * a.sl2);
+      const float alpha = exp2f(m[sub] - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[sub][kt][r] * a.sl2 - mnew);
+          s[sub][kt][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[sub] = l[sub] * alpha + rs;
+      m[sub] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[sub][dt] *= alpha;
+      pf[sub][0] = pack8(s[sub][0], s[sub][1]);
+      pf[sub][1] = pack8(s[sub][2], s[sub][3]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 vf = tr_frag<0>(Vs, ks * 32, dt * 16, lane);
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) o[sub][dt] = mfma16(vf, pf[sub][ks], o[sub][dt]);
+      }
+    if (t + 1 < nkv) sstore((t + 1) & 1);
+    __syncthreads();
+  }
+
+  bf16* Ob = a.O + b * a.bo + h * HD;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int qr = q0 + w * 32 + sub * 16 + l16;
+    if (qr >= a.Lq) continue;
+    const float inv = 1.f / l[sub];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[sub][dt][r] * inv);
+      *(bf16x4*)(Ob + (int64_t)qr * a.ldo + dt * 16 + 4 * g) = v;
+    }
+    if (g == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m[sub] + log2f(l[sub]);
+  }
+}
+
+// ============================================================================ backward ===
+// delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128)
+__global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
+                                  const bf16* __restrict__ O, int64_t ldo, int64_t bo,
+                                  float* __restrict__ delta, int B, int Lq, int H) {
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int part = threadIdx.x & 15;
+  const int64_t nrows = (int64_t)B * Lq * H;
+  float acc = 0.f;
+  int64_t b = 0, q = 0, h = 0;
+  if (row < nrows) {
+    h = row % H;
+    q = (row / H) % Lq;
+    b = row / ((int64_t)H * Lq);
+    const bf16x8 x = *(const bf16x8*)(dO + b * bdo + q * lddo + h * HD + part * 8);
+    const bf16x8 y = *(const bf16x8*)(O + b * bo + q * ldo + h * HD + part * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f(x[j]) * bf2f(y[j]);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  if (row < nrows && part == 0) delta[(b * H + h) * Lq + q] = acc;
+}
+
+// dK, dV: workgroup owns 128 keys (wave: 32 = 2 sub-tiles of 16), sweeps query tiles of 32.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 8192];  // Q tile | dO tile
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
+  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
+
+  bf16x8 kf[2][4], vf[2][4];
+  bool kvalid[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int key = k0 + w * 32 + sub * 16 + l16;
+    kvalid[sub] = key < a.k_len;
+    const int kr = min(key, a.Lk - 1);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      kf[sub][ds] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ds * 32 + g * 8);
+      vf[sub][ds] = *(const bf16x8*)(Vb + (int64_t)kr * a.ldv + ds * 32 + g * 8);
+    }
+  }
+  f32x4 dk[2][8], dv[2][8];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      dk[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dv[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  char* Qs = smem;
+  char* Ds = smem + 8192;
+  const int nq = (a.Lq + 31) / 32;
+  for (int t = 0; t < nq; ++t) {
+    const int qb = t * 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      const int qr = min(qb + row, a.Lq - 1);
+      *(u32x4*)(Qs + offB(row, ch << 4)) = *(const u32x4*)(Qb + (int64_t)qr * a.ldq + ch * 8);
+      *(u32x4*)(Ds + offB(row, ch << 4)) = *(const u32x4*)(dOb + (int64_t)qr * a.lddo + ch * 8);
+    }
+    // per-row statistics for rows q = qb + qt*16 + 4g + r
+    f32x4 lse4[2], del4[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qr = qb + qt * 16 + 4 * g + r;
+        lse4[qt][r] = qr < a.Lq ? lseb[qr] : __builtin_huge_valf();
+        del4[qt][r] = qr < a.Lq ? delb[qr] : 0.f;
+      }
+    __syncthreads();
+    bf16x8 pp[2], dsp[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4 s[2], dp[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < 4; ++ds) {
+          s[qt] = mfma16(row_frag<1>(Qs, qt * 16, ds, lane), kf[sub][ds], s[qt]);
+          dp[qt] = mfma16(row_frag<1>(Ds, qt * 16, ds, lane), vf[sub][ds], dp[qt]);
+        }
+        // s: D[q][key] with key = lane column
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = kvalid[sub] ? exp2f(s[qt][r] * a.sl2 - lse4[qt][r]) : 0.f;
+          s[qt][r] = p;
+          dp[qt][r] = p * (dp[qt][r] - del4[qt][r]);
+        }
+      }
+      pp[sub] = pack8(s[0], s[1]);
+      dsp[sub] = pack8(dp[0], dp[1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const bf16x8 dot = tr_frag<1>(Ds, 0, dt * 16, lane);
+      const bf16x8 qt_ = tr_frag<1>(Qs, 0, dt * 16, lane);
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        dv[sub][dt] = mfma16(dot, pp[sub], dv[sub][dt]);
+        dk[sub][dt] = mfma16(qt_, dsp[sub], dk[sub][dt]);
+      }
+    }
+    __syncthreads();
+  }
+  bf16* dKb = a.dK + b * a.bdk + h * HD;
+  bf16* dVb = a.dV + b * a.bdv + h * HD;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int key = k0 + w * 32 + sub * 16 + l16;
+    if (key >= a.Lk) continue;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16x4 vk, vv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        vk[r] = f2bf(dk[sub][dt][r] * a.scale);
+        vv[r] = f2bf(dv[sub][dt][r]);
+      }
+      *(bf16x4*)(dKb + (int64_t)key * a.lddk + dt * 16 + 4 * g) = vk;
+      *(bf16x4*)(dVb + (int64_t)key * a.lddv + dt * 16 + 4 * g) = vv;
+    }
+  }
+}
+
+// dQ: workgroup owns 128 queries (wave: 32), sweeps key tiles of 64.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[32768];  // K tile (image B) | V tile
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
+  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
+
+  bf16x8 qf[2][4], df[2][4];
+  float lse[2], del[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int qr = min(q0 + w * 32 + sub * 16 + l16, a.Lq - 1);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      qf[sub][ds] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ds * 32 + g * 8);
+      df[sub][ds] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ds * 32 + g * 8);
+    }
+    lse[sub] = lseb[qr];
+    del[sub] = delb[qr];
+  }
+  f32x4 dq[2][8];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) dq[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  char* Ks = smem;
+  char* Vs = smem + 16384;
+  const int nkv = (a.k_len + 63) / 64;
+  for (int t = 0; t < nkv; ++t) {
+    const int kb = t * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      const int kr = min(kb + row, a.Lk - 1);
+      *(u32x4*)(Ks + offB(row, ch << 4)) = *(const u32x4*)(Kb + (int64_t)kr * a.ldk + ch * 8);
+      *(u32x4*)(Vs + off16(row, ch)) = *(const u32x4*)(Vb + (int64_t)kr * a.ldv + ch * 8);
+    }
+    __syncthreads();
+    bf16x8 dsp[2][2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4 s[4], dp[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dp[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < 4; ++ds) {
+          s[kt] = mfma16(row_frag<1>(Ks, kt * 16, ds, lane), qf[sub][ds], s[kt]);
+          dp[kt] = mfma16(row_frag<0>(Vs, kt * 16, ds, lane), df[sub][ds], dp[kt]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb + kt * 16 + 4 * g + r;
+          const float p = key < a.k_len ? exp2f(s[kt][r] * a.sl2 - lse[sub]) : 0.f;
+          dp[kt][r] = p * (dp[kt][r] - del[sub]);
+        }
+      }
+      dsp[sub][0] = pack8(dp[0], dp[1]);
+      dsp[sub][1] = pack8(dp[2], dp[3]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 kt_ = tr_frag<1>(Ks, ks * 32, dt * 16, lane);
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) dq[sub][dt] = mfma16(kt_, dsp[sub][ks], dq[sub][dt]);
+      }
+    __syncthreads();
+  }
+  bf16* dQb = a.dQ + b * a.bdq + h * HD;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int qr = q0 + w * 32 + sub * 16 + l16;
+    if (qr >= a.Lq) continue;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[sub][dt][r] * a.scale);
+      *(bf16x4*)(dQb + (int64_t)qr * a.lddq + dt * 16 + 4 * g) = v;
+    }
+  }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+}  // namespace
+
+// o = softmax(q k^T * scale, keys >= k_len masked) v ; lse2 = log2-domain row LSE.
+extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                             int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
+                             int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
+                             int64_t Lk, int64_t H, int64_t k_len, float scale, void* stream) {
+  if (B <= 0 || Lq <= 0 || H <= 0) return 0;
+  if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || (ldq | ldk | ldv | ldo) % 8)
+    return (int)hipErrorInvalidValue;
+  AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
+             (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
+             scale * 1.4426950408889634f};
+  hipStream_t s = (hipStream_t)stream;
+  const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
+  prfl_prof::begin(kid, s);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
+  prfl_prof::end(kid, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+// dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace.
+extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                             int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
+                             int64_t ldo, int64_t bo, const void* dout, int64_t lddo, int64_t bdo,
+                             const float* lse2, float* delta, void* dq, int64_t lddq, int64_t bdq,
+                             void* dk, int64_t lddk, int64_t bdk, void* dv, int64_t lddv,
+                             int64_t bdv, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                             int64_t k_len, float scale, void* stream) {
+  if (B <= 0 || Lq <= 0 || H <= 0) return 0;
+  if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nrows = B * Lq * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((nrows + 15) / 16), dim3(256), 0, s,
+                     (const bf16*)dout, lddo, bdo, (const bf16*)o, ldo, bo, delta, (int)B, (int)Lq,
+                     (int)H);
+  PRFL_LAUNCH_CHECK();
+  AttnBwdArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
+                (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
+                bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
+                scale * 1.4426950408889634f, scale};
+  prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
+  prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
+  prfl_prof::end(KID_ATTN_BWD_DKDV, s);
+  PRFL_LAUNCH_CHECK();
+  prfl_prof::begin(KID_ATTN_BWD_DQ, s);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
+  prfl_prof::end(KID_ATTN_BWD_DQ, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}

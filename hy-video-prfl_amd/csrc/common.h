@@ -1,0 +1,104 @@
+// Shared device helpers for the MI355X (gfx950, CDNA4) PRFL kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+// round an fp32 value to the nearest bf16 and back (an autocast cast point)
+__device__ __forceinline__ float bfr(float x) { return (float)(bf16)x; }
+
+// a*b rounded to fp32 on its own (the asm barrier stops contraction into an FMA with a later
+// add), matching two separate torch ops such as `x + y * gate`.
+__device__ __forceinline__ float mul_rn(float a, float b) {
+  float p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p supplies the address of row q,
+// columns 4p..4p+3 of a 4x16 block of 16-bit elements; lane i receives column i of the 4 rows.
+__device__ __forceinline__ bf16x4 lds_read_tr(const void* lds_byte_addr) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds_byte_addr));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); red must hold NT/64 floats
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+// GELU(tanh) exactly as ATen computes it in fp32 (GeluKernel.cpp, approximate='tanh')
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
+  const float kKappa = 0.044715f;
+  float inner = kBeta * (x + kKappa * x * x * x);
+  return 0.5f * x * (1.f + tanhf(inner));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float kBeta = 0.7978845608028654f;
+  const float kKappa = 0.044715f;
+  float x_sq = x * x;
+  float inner = kBeta * (x + kKappa * x_sq * x);
+  float t = tanhf(inner);
+  float left = 0.5f * x, right = 1.f + t;
+  float left_d = 0.5f * right;
+  float right_d = left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq);
+  return left_d + right_d;
+}
+
+#define PRFL_LAUNCH_CHECK()                          \
+  do {                                               \
+    hipError_t _e = hipGetLastError();               \
+    if (_e != hipSuccess) return (int)_e;            \
+  } while (0)
+
+// per-kernel timing hooks (bench.py roofline); defined in prof.hip
+namespace prfl_prof {
+void begin(int kid, hipStream_t s);
+void end(int kid, hipStream_t s);
+void set_work(double w);  // algorithmic FLOPs/bytes of the launch being timed
+}
+enum {
+  KID_GEMM = 0, KID_ATTN_FWD, KID_ATTN_FWD_SHORT, KID_ATTN_BWD_DKDV, KID_ATTN_BWD_DQ, KID_LN, KID_RMS,
+  KID_ELTWISE, KID_ADAMW,
+  KID_COUNT
+};

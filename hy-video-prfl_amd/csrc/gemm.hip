@@ -1,0 +1,293 @@
+// bf16 MFMA GEMM for the Wan DiT projections (QKV / O / cross-attn / FFN) and their backward.
+//
+//   C[m][n] = sum_k A(m,k) * B(n,k)     (+ fused epilogue)
+//
+// Operand layouts (chosen per call so no transpose kernel is ever needed):
+//   A_KC: A(m,k) = A[m*lda + k]   (token-major activations, forward / dX)
+//  !A_KC: A(m,k) = A[k*lda + m]   (dW: A = dY^T read straight from dY [L, N])
+//   B_KC: B(n,k) = B[n*ldb + k]   (nn.Linear weight [out, in] in the forward)
+//  !B_KC: B(n,k) = B[k*ldb + n]   (dX: weight read as [out][in] with k = out; dW: X [L, in])
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16x32 tiles.
+// K-contiguous tiles live in LDS as [128 rows][64 k] (128-B rows, 16-B chunk XOR row&7) and feed
+// ds_read_b128; MN-contiguous tiles live as [64 k][128] (256-B rows, 32-B XOR (k&7)<<5) and feed
+// ds_read_b64_tr_b16 (hardware transpose), so both layouts reach the same MFMA fragment.
+// Global->LDS staging is register double-buffered: tile t+1 is loaded while tile t computes and is
+// written to the other LDS buffer after the MFMAs (one barrier per K step).
+// The MFMA is issued as D = B.A^T so each lane owns 4 consecutive n of one row m: epilogue stores
+// are 8-16 B contiguous per lane.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand per stage
+
+enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_F32 = 3, EPI_DGELU = 4 };
+
+struct GemmArgs {
+  const bf16* A; int64_t lda;
+  const bf16* B; int64_t ldb;
+  void* C; int64_t ldc;
+  int M, N, K;
+  const bf16* bias;     // [N] or null
+  const float* gate;    // [N] or null (EPI_RESID)
+  const void* res;      // EPI_RESID residual input (fp32 or bf16), may alias C
+  int64_t ldr; int res_bf16;
+  bf16* aux; int64_t ldaux;  // GELU: pre-activation out; RESID: y out; DGELU: pre-activation in
+  int accumulate;       // EPI_F32: C += acc
+};
+
+// ---- staging: global -> registers -----------------------------------------------------------
+template <bool KC>
+__device__ __forceinline__ void load_tile(u32x4 (&r)[4], const bf16* __restrict__ P, int64_t ld,
+                                          int rows, int K, int r0, int k0) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + NT * i;
+    if (KC) {  // [128 rows][8 chunks of 8 k]
+      const int row = c >> 3, kc = c & 7;
+      const int gr = min(r0 + row, rows - 1);
+      const int gk = k0 + kc * 8;
+      if (gk < K)
+        r[i] = *(const u32x4*)(P + (int64_t)gr * ld + gk);
+      else
+        r[i] = (u32x4){0u, 0u, 0u, 0u};
+    } else {   // [64 k][16 chunks of 8 rows]
+      const int kr = c >> 4, mc = c & 15;
+      const int gk = k0 + kr, gm = r0 + mc * 8;
+      if (gk < K && gm < rows)
+        r[i] = *(const u32x4*)(P + (int64_t)gk * ld + gm);
+      else
+        r[i] = (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void store_tile(char* lds, const u32x4 (&r)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + NT * i;
+    int off;
+    if (KC) {
+      const int row = c >> 3, kc = c & 7;
+      off = row * 128 + ((kc ^ (row & 7)) << 4);
+    } else {
+      const int kr = c >> 4, mc = c & 15;
+      off = kr * 256 + ((mc << 4) ^ ((kr & 7) << 5));
+    }
+    *(u32x4*)(lds + off) = r[i];
+  }
+}
+
+// fragment for MFMA 16x16x32: lane l holds X[row = base + (l&15)][k = 32*s + 8*(l>>4) + 0..7]
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int s, int lane) {
+  if (KC) {
+    const int row = base + (lane & 15);
+    const int kc = s * 4 + (lane >> 4);
+    return *(const bf16x8*)(lds + row * 128 + ((kc ^ (row & 7)) << 4));
+  } else {
+    const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+    const int col = (base + 4 * p) * 2;
+    const int k0 = s * 32 + g * 8 + q;
+    const int k1 = k0 + 4;
+    bf16x4 lo = lds_read_tr(lds + k0 * 256 + (col ^ ((k0 & 7) << 5)));
+    bf16x4 hi = lds_read_tr(lds + k1 * 256 + (col ^ ((k1 & 7) << 5)));
+    return cat8(lo, hi);
+  }
+}
+
+__device__ __forceinline__ void tile_coords(int bid, int M, int N, int& tm, int& tn) {
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  const int nwg = ntm * ntn;
+  // XCD-aware remap (bijective): blocks b, b+8, ... share an XCD; give each XCD a contiguous
+  // range of tiles so neighbouring tiles (shared A rows / B cols) hit the same L2.
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  // grouped ordering: GM tile-rows sweep all tile-columns together
+  const int GM = 8;
+  const int group = w / (GM * ntn);
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  const int within = w - group * GM * ntn;
+  tm = first_m + within % gsz;
+  tn = within / gsz;
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  // stage st: A at smem + st*2*TILE_BYTES, B right after it
+#define AS(st) (smem + (st) * 2 * TILE_BYTES)
+#define BS(st) (smem + (st) * 2 * TILE_BYTES + TILE_BYTES)
+
+  int tm, tn;
+  tile_coords(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  u32x4 ra[4], rb[4];
+  load_tile<A_KC>(ra, g.A, g.lda, g.M, g.K, m0, 0);
+  load_tile<B_KC>(rb, g.B, g.ldb, g.N, g.K, n0, 0);
+  store_tile<A_KC>(AS(0), ra);
+  store_tile<B_KC>(BS(0), rb);
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) {
+      load_tile<A_KC>(ra, g.A, g.lda, g.M, g.K, m0, (t + 1) * BK);
+      load_tile<B_KC>(rb, g.B, g.ldb, g.N, g.K, n0, (t + 1) * BK);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bfr_[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<A_KC>(AS(cur), wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr_[j] = read_frag<B_KC>(BS(cur), wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr_[j], af[i], acc[i][j]);
+    }
+    if (t + 1 < nk) {
+      store_tile<A_KC>(AS(cur ^ 1), ra);
+      store_tile<B_KC>(BS(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+
+#undef AS
+#undef BS
+  // ---- epilogue: lane owns D[n = nb + 4*(lane>>4) + r][m = mb + (lane&15)], r = 0..3 ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      f32x4 v = acc[i][j];
+      if (EPI == EPI_F32) {
+        float* cp = (float*)g.C + (int64_t)m * g.ldc + n;
+        if (g.accumulate) {
+          f32x4 o = *(f32x4*)cp;
+          v = v + o;
+        }
+        *(f32x4*)cp = v;
+        continue;
+      }
+      if (EPI == EPI_DGELU) {
+        const bf16x4 pre = *(const bf16x4*)(g.aux + (int64_t)m * g.ldaux + n);
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(bf2f(pre[r])));
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+        continue;
+      }
+      float y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + (g.bias ? bf2f(g.bias[n + r]) : 0.f));
+      if (EPI == EPI_BF16) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+      } else if (EPI == EPI_GELU) {
+        bf16x4 o, pre;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pre[r] = f2bf(y[r]);
+          o[r] = f2bf(gelu_tanh(y[r]));
+        }
+        if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+      } else if (EPI == EPI_RESID) {
+        if (g.aux) {
+          bf16x4 yo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
+          *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
+        }
+        float rv[4];
+        if (g.res_bf16) {
+          const bf16x4 rr = *(const bf16x4*)((const bf16*)g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = bf2f(rr[r]);
+        } else {
+          const f32x4 rr = *(const f32x4*)((const float*)g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = rr[r];
+        }
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = g.gate ? g.gate[n + r] : 1.f;
+          o[r] = rv[r] + mul_rn(y[r], gt);  // x + y*e (two roundings, as in torch)
+        }
+        *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
+      }
+    }
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+int launch(const GemmArgs& g, hipStream_t s) {
+  const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+                              int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                              int epilogue, const void* bias, const float* gate, const void* res,
+                              int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
+                              void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  // K is a contiguous extent only for K-major operands; MN-major operands take any K (row tail)
+  if (K <= 0 || ((a_kmajor || b_kmajor) && (K % 8) != 0) || (N % 4) != 0)
+    return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldb % 8) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  if (!a_kmajor && (M % 8)) return (int)hipErrorInvalidValue;
+  if (!b_kmajor && (N % 8)) return (int)hipErrorInvalidValue;
+  if (M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) return (int)hipErrorInvalidValue;
+  GemmArgs g{(const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, (int)M, (int)N, (int)K,
+             (const bf16*)bias, gate, res, ldr, res_bf16, (bf16*)aux, ldaux, accumulate};
+  hipStream_t s = (hipStream_t)stream;
+  prfl_prof::begin(KID_GEMM, s);
+  int rc = (int)hipErrorInvalidValue;
+#define GEMM_CASE(AK, BK_, E) \
+  if (a_kmajor == AK && b_kmajor == BK_ && epilogue == E) rc = launch<AK, BK_, E>(g, s);
+  GEMM_CASE(1, 1, EPI_BF16)
+  GEMM_CASE(1, 1, EPI_GELU)
+  GEMM_CASE(1, 1, EPI_RESID)
+  GEMM_CASE(1, 1, EPI_F32)
+  GEMM_CASE(1, 1, EPI_DGELU)
+  GEMM_CASE(1, 0, EPI_BF16)
+  GEMM_CASE(1, 0, EPI_DGELU)
+  GEMM_CASE(1, 0, EPI_F32)
+  GEMM_CASE(0, 0, EPI_F32)
+  GEMM_CASE(0, 1, EPI_F32)
+#undef GEMM_CASE
+  prfl_prof::set_work(2.0 * (double)M * (double)N * (double)K);
+  prfl_prof::end(KID_GEMM, s);
+  return rc;
+}

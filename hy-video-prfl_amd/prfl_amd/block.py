@@ -1,0 +1,284 @@
+"""Fused WanAttentionBlock forward/backward on the HIP kernels (`model.py:280-359`).
+
+The block is one autograd node (``WanBlockFn``) that implements the reference's non-reentrant
+activation checkpoint (`fsdp_utils.py:17-50`, every block checkpointed): the forward keeps only the
+block input; the backward re-runs the forward saving what the backward kernels need, then runs
+the hand-written backward chain.  fp32 master weights are cast to bf16 once per pass into
+transient buffers (q/k/v concatenated into one [3C, C] operand, so the QKV projection is a single
+GEMM without changing any state-dict key).
+
+Precision flow = the reference under bf16 autocast: LN/RMSNorm/modulation/gates
+fp32, every Linear bf16 x bf16 -> fp32 accumulate -> bf16, RoPE applied in fp32 to the bf16-rounded
+normalised q/k, residual stream fp32.
+"""
+import torch
+
+from . import ops
+from .ops import BF16, EPI_BF16, EPI_GELU, EPI_RESID, EPI_DGELU
+
+T5_CONTEXT_TOKEN_NUMBER = 512  # model.py:18
+
+SA_NAMES = ["self_attn.q.weight", "self_attn.q.bias", "self_attn.k.weight", "self_attn.k.bias",
+            "self_attn.v.weight", "self_attn.v.bias", "self_attn.o.weight", "self_attn.o.bias",
+            "self_attn.norm_q.weight", "self_attn.norm_k.weight"]
+CA_NAMES = ["norm3.weight", "norm3.bias", "cross_attn.q.weight", "cross_attn.q.bias",
+            "cross_attn.k.weight", "cross_attn.k.bias", "cross_attn.v.weight", "cross_attn.v.bias",
+            "cross_attn.o.weight", "cross_attn.o.bias", "cross_attn.norm_q.weight",
+            "cross_attn.norm_k.weight"]
+I2V_NAMES = ["cross_attn.k_img.weight", "cross_attn.k_img.bias", "cross_attn.v_img.weight",
+             "cross_attn.v_img.bias", "cross_attn.norm_k_img.weight"]
+FFN_NAMES = ["ffn.0.weight", "ffn.0.bias", "ffn.2.weight", "ffn.2.bias"]
+
+
+def param_names(i2v):
+    return SA_NAMES + CA_NAMES + (I2V_NAMES if i2v else []) + FFN_NAMES
+
+
+class Meta:
+    """Non-tensor block arguments."""
+
+    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6):
+        self.num_heads = num_heads
+        self.grid = grid            # list of (F, H, W) per sample
+        self.seq_len = seq_len      # list of valid key lengths per sample (k_lens)
+        self.rope_tab = rope_tab    # fp32 [1024, 64, 2] device tensor
+        self.i2v = i2v
+        self.eps = eps
+
+
+class BF16Weights:
+    """bf16 copies of a block's Linear weights/biases for one forward or backward pass."""
+
+    def __init__(self, P):
+        g = P.__getitem__
+        C = g("self_attn.q.weight").shape[0]
+        dev = g("self_attn.q.weight").device
+        self.wqkv = torch.empty(3 * C, C, dtype=BF16, device=dev)
+        self.bqkv = torch.empty(3 * C, dtype=BF16, device=dev)
+        for i, n in enumerate("qkv"):
+            ops.cast_bf16(g(f"self_attn.{n}.weight"), self.wqkv[i * C:(i + 1) * C])
+            ops.cast_bf16(g(f"self_attn.{n}.bias"), self.bqkv[i * C:(i + 1) * C])
+        c = lambda n: ops.cast_bf16(g(n))  # noqa: E731
+        self.wo, self.bo = c("self_attn.o.weight"), c("self_attn.o.bias")
+        for n in ("q", "k", "v", "o", "k_img", "v_img"):
+            key = f"cross_attn.{n}.weight"
+            if key in P:
+                setattr(self, "wc" + n, c(key))
+                setattr(self, "bc" + n, c(f"cross_attn.{n}.bias"))
+        self.w1, self.b1 = c("ffn.0.weight"), c("ffn.0.bias")
+        self.w2, self.b2 = c("ffn.2.weight"), c("ffn.2.bias")
+
+
+def _split_ctx(ctx, i2v):
+    if not i2v:
+        return ctx, None
+    n_img = ctx.shape[0] - T5_CONTEXT_TOKEN_NUMBER
+    return ctx[n_img:], ctx[:n_img]
+
+
+def block_forward_one(P, W, x, e, ctx, meta, b, save):
+    """One sample: x [L, C] (fp32, or bf16 for block 0), e [6, C] fp32, ctx [Lc, C] bf16."""
+    g = P.__getitem__
+    L, C = x.shape
+    nh, eps = meta.num_heads, meta.eps
+    S = {}
+    # ---- self-attention (model.py:344-348) ----
+    h1, m1, r1 = ops.ln_mod_fwd(x, scale=e[1], shift=e[0], eps=eps)
+    qkv = ops.linear(h1, W.wqkv, W.bqkv)
+    q_raw, k_raw, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    grid = meta.grid[b]
+    qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid)
+    kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
+    ao, lse = ops.attn_fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
+    y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
+    x1 = ops.linear(ao, W.wo, W.bo, EPI_RESID, gate=e[2], res=x, aux=y1)
+    if save:
+        S.update(h1=h1, m1=m1, r1=r1, qkv=qkv, qr=qr, rq=rq, kr=kr, rk=rk, ao=ao, lse=lse, y1=y1,
+                 x1=x1)
+    else:
+        del h1, qkv, qr, kr, ao
+    # ---- cross-attention (model.py:352, :204-271) ----
+    n3, m3, r3 = ops.ln_mod_fwd(x1, w=g("norm3.weight"), b=g("norm3.bias"), eps=eps)
+    qc_raw = ops.linear(n3, W.wcq, W.bcq)
+    qc, rqc = ops.rms_rope_fwd(qc_raw, g("cross_attn.norm_q.weight"), eps)
+    ctx_t, ctx_i = _split_ctx(ctx, meta.i2v)
+    kc_raw = ops.linear(ctx_t, W.wck, W.bck)
+    kc, rkc = ops.rms_rope_fwd(kc_raw, g("cross_attn.norm_k.weight"), eps)
+    vc = ops.linear(ctx_t, W.wcv, W.bcv)
+    ac, lsec = ops.attn_fwd(qc, kc, vc, nh)
+    if meta.i2v:
+        ki_raw = ops.linear(ctx_i, W.wck_img, W.bck_img)
+        ki, rki = ops.rms_rope_fwd(ki_raw, g("cross_attn.norm_k_img.weight"), eps)
+        vi = ops.linear(ctx_i, W.wcv_img, W.bcv_img)
+        ai, lsei = ops.attn_fwd(qc, ki, vi, nh)
+        acs = ac + ai          # fp32 sum of two bf16 outputs, rounded once (model.py:269)
+    else:
+        acs = ac
+    x2 = x1 if not save else torch.empty_like(x1)
+    ops.linear(acs, W.wco, W.bco, EPI_RESID, out=x2, res=x1)
+    if save:
+        S.update(n3=n3, m3=m3, r3=r3, qc_raw=qc_raw, qc=qc, rqc=rqc, kc_raw=kc_raw, kc=kc, rkc=rkc,
+                 vc=vc, ac=ac, lsec=lsec, acs=acs, x2=x2)
+        if meta.i2v:
+            S.update(ki_raw=ki_raw, ki=ki, rki=rki, vi=vi, ai=ai, lsei=lsei)
+    # ---- FFN (model.py:353-355) ----
+    h2, m2, r2 = ops.ln_mod_fwd(x2, scale=e[4], shift=e[3], eps=eps)
+    fpre = torch.empty(L, W.w1.shape[0], dtype=BF16, device=x.device) if save else None
+    fact = ops.linear(h2, W.w1, W.b1, EPI_GELU, aux=fpre)
+    y2 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
+    out = torch.empty_like(x2) if save else x2
+    ops.linear(fact, W.w2, W.b2, EPI_RESID, out=out, gate=e[5], res=x2, aux=y2)
+    if save:
+        S.update(h2=h2, m2=m2, r2=r2, fpre=fpre, fact=fact, y2=y2)
+    return out, S
+
+
+def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
+    """Backward of block_forward_one.  dout fp32 [L, C] (consumed/overwritten).  Parameter
+    gradients are accumulated into the fp32 dict G; returns (dx fp32, de [6, C], dctx fp32)."""
+    g = P.__getitem__
+    L, C = x.shape
+    nh, eps = meta.num_heads, meta.eps
+    grid = meta.grid[b]
+    de = [None] * 6
+
+    def acc(name, val):
+        if G.get(name) is None:
+            G[name] = val
+        else:
+            G[name].add_(val)
+
+    def dw(name, dy, xin):
+        if G.get(name) is None:
+            G[name] = ops.linear_dw(dy, xin)
+        else:
+            ops.linear_dw(dy, xin, out=G[name], accumulate=True)
+
+    dx = dout
+    # ---- FFN ----
+    dy2, de[5], db2 = ops.gate_bwd(dx, S["y2"], e[5])
+    acc("ffn.2.bias", db2)
+    dw("ffn.2.weight", dy2, S["fact"])
+    dfpre = ops.linear_dx(dy2, W.w2, epilogue=EPI_DGELU, aux=S["fpre"])
+    del dy2
+    dw("ffn.0.weight", dfpre, S["h2"])
+    acc("ffn.0.bias", ops.colsum(dfpre))
+    dh2 = ops.linear_dx(dfpre, W.w1)
+    del dfpre
+    de[4], de[3] = ops.ln_mod_bwd(dh2, S["x2"], S["m2"], S["r2"], dx, scale=e[4])
+    del dh2
+    # ---- cross-attention ----
+    dyc, _, dbco = ops.gate_bwd(dx, None, None, want_gate=False)
+    acc("cross_attn.o.bias", dbco)
+    dw("cross_attn.o.weight", dyc, S["acs"])
+    dac = ops.linear_dx(dyc, W.wco)
+    del dyc
+    ctx_t, ctx_i = _split_ctx(ctx, meta.i2v)
+    dqc, dkc, dvc = ops.attn_bwd(S["qc"], S["kc"], S["vc"], S["ac"], dac, S["lsec"], nh)
+    if meta.i2v:
+        dqi, dki, dvi = ops.attn_bwd(S["qc"], S["ki"], S["vi"], S["ai"], dac, S["lsei"], nh)
+        dqc = dqc + dqi
+    dqc_raw, dnq = ops.rms_rope_bwd(dqc, S["qc_raw"], S["rqc"], g("cross_attn.norm_q.weight"))
+    acc("cross_attn.norm_q.weight", dnq)
+    dw("cross_attn.q.weight", dqc_raw, S["n3"])
+    acc("cross_attn.q.bias", ops.colsum(dqc_raw))
+    dn3 = ops.linear_dx(dqc_raw, W.wcq)
+    dw3, db3 = ops.ln_mod_bwd(dn3, S["x1"], S["m3"], S["r3"], dx, w=g("norm3.weight"))
+    acc("norm3.weight", dw3)
+    acc("norm3.bias", db3)
+    del dn3, dqc_raw
+    dkc_raw, dnk = ops.rms_rope_bwd(dkc, S["kc_raw"], S["rkc"], g("cross_attn.norm_k.weight"))
+    acc("cross_attn.norm_k.weight", dnk)
+    dw("cross_attn.k.weight", dkc_raw, ctx_t)
+    acc("cross_attn.k.bias", ops.colsum(dkc_raw))
+    dw("cross_attn.v.weight", dvc, ctx_t)
+    acc("cross_attn.v.bias", ops.colsum(dvc))
+    dctx = torch.empty(ctx.shape, dtype=torch.float32, device=x.device)
+    n_img = ctx.shape[0] - ctx_t.shape[0]
+    dctx_t = dctx[n_img:]
+    ops.gemm(dkc_raw, W.wck, dctx_t, ctx_t.shape[0], C, C, True, False, ops.EPI_F32)
+    ops.gemm(dvc, W.wcv, dctx_t, ctx_t.shape[0], C, C, True, False, ops.EPI_F32, accumulate=True)
+    if meta.i2v:
+        dki_raw, dnki = ops.rms_rope_bwd(dki, S["ki_raw"], S["rki"],
+                                         g("cross_attn.norm_k_img.weight"))
+        acc("cross_attn.norm_k_img.weight", dnki)
+        dw("cross_attn.k_img.weight", dki_raw, ctx_i)
+        acc("cross_attn.k_img.bias", ops.colsum(dki_raw))
+        dw("cross_attn.v_img.weight", dvi, ctx_i)
+        acc("cross_attn.v_img.bias", ops.colsum(dvi))
+        dctx_i = dctx[:n_img]
+        ops.gemm(dki_raw, W.wck_img, dctx_i, n_img, C, C, True, False, ops.EPI_F32)
+        ops.gemm(dvi, W.wcv_img, dctx_i, n_img, C, C, True, False, ops.EPI_F32, accumulate=True)
+    # ---- self-attention ----
+    dy1, de[2], dbo = ops.gate_bwd(dx, S["y1"], e[2])
+    acc("self_attn.o.bias", dbo)
+    dw("self_attn.o.weight", dy1, S["ao"])
+    dao = ops.linear_dx(dy1, W.wo)
+    del dy1
+    qkv = S["qkv"]
+    dqkv = torch.empty(L, 3 * C, dtype=BF16, device=x.device)
+    dqr, dkr, _ = ops.attn_bwd(S["qr"], S["kr"], qkv[:, 2 * C:], S["ao"], dao, S["lse"], nh,
+                               k_len=meta.seq_len[b], dv=dqkv[:, 2 * C:])
+    del dao
+    _, dnq = ops.rms_rope_bwd(dqr, qkv[:, :C], S["rq"], g("self_attn.norm_q.weight"),
+                              meta.rope_tab, grid, dx=dqkv[:, :C])
+    _, dnk = ops.rms_rope_bwd(dkr, qkv[:, C:2 * C], S["rk"], g("self_attn.norm_k.weight"),
+                              meta.rope_tab, grid, dx=dqkv[:, C:2 * C])
+    acc("self_attn.norm_q.weight", dnq)
+    acc("self_attn.norm_k.weight", dnk)
+    del dqr, dkr
+    for i, n in enumerate("qkv"):
+        dw(f"self_attn.{n}.weight", dqkv[:, i * C:(i + 1) * C], S["h1"])
+    dbqkv = ops.colsum(dqkv)
+    for i, n in enumerate("qkv"):
+        acc(f"self_attn.{n}.bias", dbqkv[i * C:(i + 1) * C].clone())
+    dh1 = ops.gemm(dqkv, W.wqkv, torch.empty(L, C, dtype=BF16, device=x.device), L, C, 3 * C,
+                   True, False, EPI_BF16)
+    del dqkv
+    de[1], de[0] = ops.ln_mod_bwd(dh1, x, S["m1"], S["r1"], dx, scale=e[1])
+    return dx, torch.stack(de), dctx
+
+
+class WanBlockFn(torch.autograd.Function):
+    """Checkpointed fused block: forward(x [B,L,C], e [B,6,C], ctx [B,Lc,C] bf16, *params)."""
+
+    @staticmethod
+    def forward(fctx, x, e, context, meta, names, *params):
+        P = dict(zip(names, params))
+        W = BF16Weights(P)
+        outs = []
+        for b in range(x.shape[0]):
+            o, _ = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False)
+            outs.append(o)
+        del W
+        fctx.meta, fctx.names = meta, names
+        fctx.save_for_backward(x, e, context, *params)
+        return torch.stack(outs)
+
+    @staticmethod
+    def backward(fctx, dout):
+        x, e, context, *params = fctx.saved_tensors
+        meta, names = fctx.meta, fctx.names
+        P = dict(zip(names, params))
+        W = BF16Weights(P)
+        G = {}
+        dxs, des, dcs = [], [], []
+        for b in range(x.shape[0]):
+            _, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=True)
+            d = dout[b].to(torch.float32).contiguous().clone()
+            dx, de, dc = block_backward_one(P, W, x[b], e[b], context[b], meta, b, S, d, G)
+            del S
+            dxs.append(dx)
+            des.append(de)
+            dcs.append(dc)
+        dx = torch.stack(dxs).to(x.dtype)
+        de = torch.stack(des)
+        dctx = torch.stack(dcs).to(context.dtype) if context.requires_grad else None
+        pg = [G.get(n) if p.requires_grad else None for n, p in zip(names, params)]
+        return (dx, de, dctx, None, None, *pg)
+
+
+def block_apply(P, x, e, context, meta):
+    """P: ordered dict name -> fp32 parameter (the block's, without 'modulation')."""
+    names = tuple(P.keys())
+    return WanBlockFn.apply(x, e, context, meta, names, *P.values())

@@ -1,0 +1,238 @@
+"""Tensor-level wrappers over the C ABI (shapes, strides and dtypes checked here).
+
+All tensors are 2-D row-major views ``[rows, cols]`` with unit column stride; row strides are
+passed through, so q/k/v slices of the fused QKV output need no copy.
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import I32, I64, F32, call, ptr, stream_ptr
+
+BF16 = torch.bfloat16
+EPI_BF16, EPI_GELU, EPI_RESID, EPI_F32, EPI_DGELU = range(5)
+
+
+def _ld(t):
+    assert t.dim() == 2 and t.stride(1) == 1, (tuple(t.shape), t.stride())
+    return t.stride(0)
+
+
+def gemm(a, b, c, M, N, K, a_kmajor=True, b_kmajor=True, epilogue=EPI_BF16, bias=None,
+         gate=None, res=None, aux=None, accumulate=False):
+    """C[m][n] = sum_k A(m,k) B(n,k) (+ epilogue); see include/prfl_hip.h."""
+    _lib.require_gpu(a, b, c)
+    assert a.dtype == BF16 and b.dtype == BF16
+    assert bias is None or (bias.dtype == BF16 and bias.is_contiguous())
+    assert gate is None or (gate.dtype == torch.float32 and gate.is_contiguous())
+    call("prfl_gemm_bf16", ptr(a), I64(_ld(a)), I32(int(a_kmajor)), ptr(b), I64(_ld(b)),
+         I32(int(b_kmajor)), ptr(c), I64(_ld(c)), I64(M), I64(N), I64(K), I32(epilogue),
+         ptr(bias), ptr(gate), ptr(res), I64(_ld(res) if res is not None else 0),
+         I32(int(res is not None and res.dtype == BF16)), ptr(aux),
+         I64(_ld(aux) if aux is not None else 0), I32(int(accumulate)), stream_ptr())
+    return c
+
+
+def linear(x, w, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None, aux=None):
+    """y = x @ w^T (+bias) with x [M,K] bf16, w [N,K] bf16 (nn.Linear layout)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        dt = torch.float32 if epilogue in (EPI_RESID, EPI_F32) else BF16
+        out = torch.empty(M, N, dtype=dt, device=x.device)
+    return gemm(x, w, out, M, N, K, True, True, epilogue, bias, gate, res, aux)
+
+
+def linear_dx(dy, w, out=None, epilogue=EPI_BF16, aux=None):
+    """dX[M,K] = dY[M,N] @ W[N,K] (bf16 out; DGELU epilogue multiplies by gelu'(aux))."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=BF16, device=dy.device)
+    return gemm(dy, w, out, M, K, N, True, False, epilogue, aux=aux)
+
+
+def linear_dw(dy, x, out=None, accumulate=False):
+    """dW[N,K] = dY[M,N]^T @ X[M,K] in fp32 (accumulate=True adds into `out`)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if out is None:
+        out = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+    return gemm(dy, x, out, N, K, M, False, False, EPI_F32, accumulate=accumulate)
+
+
+def cast_bf16(src, dst=None):
+    """fp32 -> bf16 (round to nearest even); dst may be a contiguous slice of a larger buffer."""
+    _lib.require_gpu(src)
+    src = src.contiguous()
+    if dst is None:
+        dst = torch.empty(src.shape, dtype=BF16, device=src.device)
+    assert dst.is_contiguous() and dst.numel() == src.numel()
+    call("prfl_cast_f32_bf16", ptr(src), ptr(dst), I64(src.numel()), stream_ptr())
+    return dst
+
+
+def colsum_reduce(part, out=None, accumulate=False):
+    P_, N = part.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=part.device)
+        accumulate = False
+    call("prfl_colsum_reduce", ptr(part), I64(P_), I64(N), ptr(out), I32(int(accumulate)),
+         stream_ptr())
+    return out
+
+
+def colsum(x, out=None, accumulate=False):
+    """sum over rows of a bf16 [L, N] matrix -> fp32 [N]."""
+    L, N = x.shape
+    rp = call_int("prfl_colsum_rows_per_part")
+    part = torch.empty((L + rp - 1) // rp, N, dtype=torch.float32, device=x.device)
+    call("prfl_colsum_bf16", ptr(x), I64(_ld(x)), I64(L), I64(N), ptr(part), stream_ptr())
+    return colsum_reduce(part, out, accumulate)
+
+
+_int_cache = {}
+
+
+def call_int(name):
+    if name not in _int_cache:
+        _int_cache[name] = getattr(_lib.load(), name)()
+    return _int_cache[name]
+
+
+def gate_bwd(dx, y, gate, dy_out=None, want_gate=True, want_bias=True):
+    """x_out = x + y*gate: dy = bf16(dx*gate), d gate = sum dx*y, d bias = sum dy."""
+    L, N = dx.shape
+    rp = call_int("prfl_colsum_rows_per_part")
+    nb = (L + rp - 1) // rp
+    if dy_out is None:
+        dy_out = torch.empty(L, N, dtype=BF16, device=dx.device)
+    pg = torch.empty(nb, N, dtype=torch.float32, device=dx.device) if (want_gate and y is not None) else None
+    pb = torch.empty(nb, N, dtype=torch.float32, device=dx.device) if want_bias else None
+    call("prfl_gate_bwd", ptr(dx), I64(_ld(dx)), ptr(y), I64(_ld(y) if y is not None else 0),
+         ptr(gate), I64(L), I64(N), ptr(dy_out), I64(_ld(dy_out)), ptr(pg), ptr(pb), stream_ptr())
+    dgate = colsum_reduce(pg) if pg is not None else None
+    dbias = colsum_reduce(pb) if pb is not None else None
+    return dy_out, dgate, dbias
+
+
+def ln_mod_fwd(x, scale=None, shift=None, w=None, b=None, eps=1e-6, out=None):
+    """bf16(LN(x)*(1+scale)+shift) or bf16(LN(x)*w+b); returns (out, mean, rstd)."""
+    L, C = x.shape
+    if out is None:
+        out = torch.empty(L, C, dtype=BF16, device=x.device)
+    mean = torch.empty(L, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(L, dtype=torch.float32, device=x.device)
+    call("prfl_ln_mod_fwd", ptr(x), I32(int(x.dtype == BF16)), I64(_ld(x)), I64(L), I64(C),
+         ptr(scale), ptr(shift), ptr(w), ptr(b), F32(eps), ptr(out), I64(_ld(out)), ptr(mean),
+         ptr(rstd), stream_ptr())
+    return out, mean, rstd
+
+
+def ln_mod_bwd(dy, x, mean, rstd, dx, scale=None, w=None, accumulate=True):
+    """dx (+)= LN backward; returns (sum dy*xhat, sum dy) — (d scale, d shift) or (d w, d b)."""
+    L, C = x.shape
+    rp = call_int("prfl_norm_rows_per_part")
+    nb = (L + rp - 1) // rp
+    p0 = torch.empty(nb, C, dtype=torch.float32, device=x.device)
+    p1 = torch.empty(nb, C, dtype=torch.float32, device=x.device)
+    call("prfl_ln_mod_bwd", ptr(dy), I64(_ld(dy)), ptr(x), I32(int(x.dtype == BF16)), I64(_ld(x)),
+         ptr(mean), ptr(rstd), I64(L), I64(C), ptr(scale), ptr(w), ptr(dx), I64(_ld(dx)),
+         I32(int(accumulate)), ptr(p0), ptr(p1), stream_ptr())
+    return colsum_reduce(p0), colsum_reduce(p1)
+
+
+def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None):
+    L, C = x.shape
+    if out is None:
+        out = torch.empty(L, C, dtype=BF16, device=x.device)
+    rstd = torch.empty(L, dtype=torch.float32, device=x.device)
+    f, h, ww = grid
+    call("prfl_rms_rope_fwd", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps), ptr(rope_tab),
+         I64(f), I64(h), I64(ww), ptr(out), I64(_ld(out)), ptr(rstd), stream_ptr())
+    return out, rstd
+
+
+def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None):
+    """returns (dx bf16, d w fp32)."""
+    L, C = x.shape
+    rp = call_int("prfl_norm_rows_per_part")
+    p0 = torch.empty((L + rp - 1) // rp, C, dtype=torch.float32, device=x.device)
+    if dx is None:
+        dx = torch.empty(L, C, dtype=BF16, device=x.device)
+    f, h, ww = grid
+    call("prfl_rms_rope_bwd", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd), I64(L),
+         I64(C), ptr(w), ptr(rope_tab), I64(f), I64(h), I64(ww), ptr(dx), I64(_ld(dx)), ptr(p0),
+         stream_ptr())
+    return dx, colsum_reduce(p0)
+
+
+def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None):
+    """q [Lq, H*128], k/v [Lk, H*128] (row-strided views) -> (o bf16 [Lq, H*128], lse2 [H, Lq])."""
+    Lq, C = q.shape
+    Lk = k.shape[0]
+    assert C == num_heads * 128, "head_dim must be 128"
+    k_len = Lk if k_len is None else int(k_len)
+    sc = scale if scale is not None else 1.0 / math.sqrt(128)
+    if out is None:
+        out = torch.empty(Lq, C, dtype=BF16, device=q.device)
+    lse = torch.empty(num_heads, Lq, dtype=torch.float32, device=q.device)
+    call("prfl_attn_fwd", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
+         I64(_ld(v)), I64(0), ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk),
+         I64(num_heads), I64(k_len), F32(sc), stream_ptr())
+    return out, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=None, scale=None):
+    Lq, C = q.shape
+    Lk = k.shape[0]
+    k_len = Lk if k_len is None else int(k_len)
+    sc = scale if scale is not None else 1.0 / math.sqrt(128)
+    dev = q.device
+    dq = torch.empty(Lq, C, dtype=BF16, device=dev) if dq is None else dq
+    dk = torch.empty(Lk, C, dtype=BF16, device=dev) if dk is None else dk
+    dv = torch.empty(Lk, C, dtype=BF16, device=dev) if dv is None else dv
+    delta = torch.empty(num_heads, Lq, dtype=torch.float32, device=dev)
+    call("prfl_attn_bwd", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
+         I64(_ld(v)), I64(0), ptr(o), I64(_ld(o)), I64(0), ptr(do), I64(_ld(do)), I64(0), ptr(lse),
+         ptr(delta), ptr(dq), I64(_ld(dq)), I64(0), ptr(dk), I64(_ld(dk)), I64(0), ptr(dv),
+         I64(_ld(dv)), I64(0), I64(1), I64(Lq), I64(Lk), I64(num_heads), I64(k_len), F32(sc),
+         stream_ptr())
+    return dq, dk, dv
+
+
+def sumsq_(x, out):
+    call("prfl_sumsq", ptr(x), I64(x.numel()), ptr(out), stream_ptr())
+
+
+def scale_(x, factor):
+    call("prfl_scale", ptr(x), I64(x.numel()), ptr(factor), stream_ptr())
+
+
+def adamw_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step):
+    for t in (p, g, m, v):
+        assert t.is_contiguous() and t.dtype == torch.float32
+    call("prfl_adamw", ptr(p), ptr(g), ptr(m), ptr(v), I64(p.numel()), F32(lr), F32(beta1),
+         F32(beta2), F32(eps), F32(weight_decay), I64(step), stream_ptr())
+
+
+def rope_table(freqs_complex, device):
+    """complex freqs [1024, 64] (model.py:521-526) -> fp32 (cos, sin) table on device."""
+    t = torch.view_as_real(freqs_complex.to(torch.complex128)).to(torch.float32).contiguous()
+    return t.to(device)
+
+
+def prof_enable(on=True):
+    call("prfl_prof_enable", I32(int(on)))
+
+
+def prof_collect():
+    import ctypes
+    n = _lib.NKID
+    counts = (ctypes.c_int64 * n)()
+    ms = (ctypes.c_double * n)()
+    work = (ctypes.c_double * n)()
+    call("prfl_prof_collect", ctypes.cast(counts, ctypes.c_void_p), ctypes.cast(ms, ctypes.c_void_p),
+         ctypes.cast(work, ctypes.c_void_p), I32(n))
+    return {k: dict(count=counts[i], ms=ms[i], work=work[i]) for k, i in _lib.KID.items()}

@@ -1,0 +1,120 @@
+/*
+ * prfl_hip.h — C ABI of the MI355X-native (gfx950 / CDNA4) PRFL hot-path kernels.
+ *
+ * Library: hy-video-prfl_amd/prfl_amd/lib/libprfl_hip.so   (built by `make -C hy-video-prfl_amd`)
+ *
+ * Conventions (every entry point):
+ *   - all tensors are caller-owned device pointers (PyTorch caching allocator or hipMalloc);
+ *     kernels never allocate, never synchronise, and are stream-ordered on `stream`
+ *     (a hipStream_t passed as void*; NULL = the default stream);
+ *   - sizes and leading dimensions are in ELEMENTS; bf16 = IEEE bfloat16 bit pattern (uint16);
+ *   - return 0 on success, otherwise a hipError_t code (hipErrorInvalidValue = 1 for bad
+ *     shapes/alignment).  The Python layer turns non-zero into RuntimeError.
+ *   - stateless and re-entrant except the optional profiling hooks (prfl_prof_*), which are
+ *     single-threaded host state.
+ *
+ * Each function names the reference interface it replaces (paths relative to the
+ * Tencent-Hunyuan/HY-Video-PRFL tree).
+ */
+#ifndef PRFL_HIP_H
+#define PRFL_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- GEMM -------------------------------------------------------------------------------
+ * Replaces the autocast nn.Linear calls of the DiT block and their autograd backward:
+ *   diffusers_lite/wan/modules/model.py:156-159,175-177,200 (self-attn q/k/v/o),
+ *   :216-225,257-270 (cross-attn q/k/v/o, k_img/v_img), :313-315 (FFN), :499-505 (embeddings).
+ * C[m][n] = sum_k A(m,k) B(n,k) with
+ *   A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];   B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
+ * epilogue: 0 BF16   C = bf16(acc + bias)                              (bias bf16 [N] or NULL)
+ *           1 GELU   C = bf16(gelu_tanh(bf16(acc+bias))); aux (opt.) = bf16(acc+bias)
+ *           2 RESID  C(f32) = res + bf16(acc+bias) * gate[n]; aux (opt.) = bf16(acc+bias)
+ *                    (res fp32 or bf16 per res_bf16, may alias C; gate fp32 [N] or NULL = 1)
+ *           3 F32    C(f32) = acc (+ C if accumulate)                  (weight gradients)
+ *           4 DGELU  C = bf16(bf16(acc) * gelu_tanh'(aux))              (aux = pre-activation)
+ * Requires K % 8 == 0, N % 4 == 0, lda/ldb % 8 == 0, 16-B aligned A/B, and the contiguous
+ * extent of an MN-major operand a multiple of 8. */
+int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+                   int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                   int epilogue, const void* bias, const float* gate, const void* res,
+                   int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
+                   void* stream);
+
+/* ---- attention ---------------------------------------------------------------------------
+ * Replaces flash_attn.flash_attn_varlen_func at diffusers_lite/wan/modules/attention.py:96-127
+ * (called from model.py:188, :221, :262, :264) for head_dim 128, non-causal, no dropout.
+ * q/k/v/o are [B][L][H*128] with row stride ld* and batch stride b*; keys >= k_len are masked
+ * (the `k_lens=seq_lens` of model.py:191).  lse2 [B][H][Lq] = log2-domain log-sum-exp
+ * (max*scale*log2e + log2(sum)), consumed by prfl_attn_bwd. */
+int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
+                  const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
+                  float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
+                  float scale, void* stream);
+/* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
+ * caller-owned workspace. */
+int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
+                  const void* v, int64_t ldv, int64_t bv, const void* o, int64_t ldo, int64_t bo,
+                  const void* dout, int64_t lddo, int64_t bdo, const float* lse2, float* delta,
+                  void* dq, int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
+                  void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq, int64_t Lk,
+                  int64_t H, int64_t k_len, float scale, void* stream);
+
+/* ---- normalisation ----------------------------------------------------------------------
+ * WanLayerNorm + AdaLN modulation (model.py:125-135, :345, :353):
+ *   out = bf16(LN(x) * (1 + scale) + shift)     (w == NULL; LN rounded to bf16 if x_bf16)
+ * or the affine norm3 (model.py:304-306, :352):  out = bf16(LN(x) * w + b).
+ * x is fp32 or bf16 [L][ldx]; mean/rstd [L] fp32 are saved for the backward.  C <= 5120. */
+int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L, int64_t C,
+                    const float* scale, const float* shift, const float* w, const float* b,
+                    float eps, void* out, int64_t ldo, float* mean, float* rstd, void* stream);
+/* dx (+)= LN backward of dy (bf16); part0/part1 [ceil(L/prfl_norm_rows_per_part())][C] receive
+ * partial column sums of dy*xhat (d scale | d w) and dy (d shift | d b). */
+int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int x_bf16, int64_t ldx,
+                    const float* mean, const float* rstd, int64_t L, int64_t C,
+                    const float* scale, const float* w, float* dx, int64_t lddx,
+                    int dx_accumulate, float* part0, float* part1, void* stream);
+int prfl_norm_rows_per_part(void);
+
+/* WanRMSNorm (model.py:106-122) over all C channels + optional 3-D RoPE (rope_apply,
+ * model.py:61-103; rope_tab = fp32 (cos,sin) [1024][64] of the complex freqs of model.py:521-526,
+ * grid (F,Hg,Wg); rows >= F*Hg*Wg are not rotated; rope_tab == NULL -> no RoPE).
+ *   out = bf16(rope(bf16(x * rsqrt(mean(x^2)+eps)) * w)) */
+int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w, float eps,
+                      const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* out,
+                      int64_t ldo, float* rstd, void* stream);
+int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
+                      const float* rstd, int64_t L, int64_t C, const float* w,
+                      const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
+                      int64_t lddx, float* part0, void* stream);
+
+/* ---- element-wise / reductions ------------------------------------------------------------ */
+/* autocast weight cast fp32 -> bf16 (the .to(bf16) of every Linear weight under autocast). */
+int prfl_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
+/* backward of the gated residual x + y*gate (model.py:348, :355): dy = bf16(dx*gate);
+ * partial column sums of dx*y (-> d gate) and of dy (-> d bias of the producing Linear). */
+int prfl_gate_bwd(const float* dx, int64_t lddx, const void* y, int64_t ldy, const float* gate,
+                  int64_t L, int64_t N, void* dy, int64_t lddy, float* pgate, float* pbias,
+                  void* stream);
+int prfl_colsum_bf16(const void* x, int64_t ld, int64_t L, int64_t N, float* part, void* stream);
+int prfl_colsum_reduce(const float* part, int64_t P, int64_t N, float* out, int accumulate,
+                       void* stream);
+int prfl_colsum_rows_per_part(void);
+/* grad-norm clipping pieces of transformer.clip_grad_norm_ (train_prfl.py:825, :972) */
+int prfl_sumsq(const float* x, int64_t n, float* out, void* stream);
+int prfl_scale(float* x, int64_t n, const float* factor, void* stream);
+/* torch.optim.AdamW step (train_prfl.py:485-491, :827-830) on one fp32 tensor. */
+int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+               float beta2, float eps, float weight_decay, int64_t step, void* stream);
+
+/* ---- profiling (bench.py roofline) -------------------------------------------------------- */
+int prfl_prof_enable(int on);
+int prfl_prof_collect(int64_t* counts, double* ms, double* work, int nkid);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRFL_HIP_H */

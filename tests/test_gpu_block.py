@@ -1,0 +1,99 @@
+"""Fused WanAttentionBlock (HIP path) vs the oracle and the reference golden fixtures.
+
+Tolerances: block output rel-L2 <= 1e-2, input / parameter grads rel-L2 <= 3e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+import seeded
+from shapes import block_shapes, seeded_params
+from oracle import wan_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().flatten()
+    b = torch.as_tensor(b).detach().double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def run_block(P, x, e, ctx, grid, seq_len, nh, i2v, up):
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    mod = P["blocks.0.modulation"]
+    names = [n for n in B.param_names(i2v)]
+    Pd = {n: P["blocks.0." + n].detach().to(DEV).requires_grad_(True) for n in names}
+    xd = x.detach().to(DEV).requires_grad_(True)
+    e0d = e.detach().to(DEV).requires_grad_(True)
+    modd = mod.detach().to(DEV).requires_grad_(True)
+    ctxd = ctx.detach().to(DEV).to(torch.bfloat16).requires_grad_(True)
+    meta = B.Meta(nh, [grid], [seq_len], ops.rope_table(O.rope_freqs(128), DEV), i2v)
+    out = B.block_apply(Pd, xd, modd + e0d, ctxd, meta)
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    return out, xd.grad, e0d.grad, modd.grad, ctxd.grad, {n: p.grad for n, p in Pd.items()}
+
+
+@pytest.mark.parametrize("i2v,x_bf16", [(False, False), (True, False), (False, True)])
+def test_toy_block_vs_oracle(i2v, x_bf16):
+    dim, ffn, nh = 256, 512, 2
+    P = seeded_params(block_shapes("blocks.0.", dim, ffn, i2v), prefix="tb.")
+    L, Lc = 105, (512 if not i2v else 769)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1, L, dim, generator=g)
+    if x_bf16:
+        x = x.to(torch.bfloat16)
+    e = torch.randn(1, 6, dim, generator=g) * 0.1
+    ctx = torch.randn(1, Lc, dim, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, dim, generator=g)
+    grid = (3, 5, 7)
+    out, dx, de, dmod, dctx, G = run_block(P, x, e, ctx, grid, L, nh, i2v, up)
+    # oracle
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    xr = (x.clone() if x_bf16 else x.clone()).requires_grad_(True)
+    er = e.clone().requires_grad_(True)
+    cr = ctx.float().requires_grad_(True)
+    ref = O.block_forward(Pr, "blocks.0.", xr, er, torch.tensor([grid]), O.rope_freqs(128), cr,
+                          nh, seq_len=L, i2v=i2v)
+    (ref * up).sum().backward()
+    assert rel(out, ref) < 1e-2, rel(out, ref)
+    assert rel(dx.float(), xr.grad.float()) < 3e-2, rel(dx.float(), xr.grad.float())
+    assert rel(de, er.grad) < 3e-2, rel(de, er.grad)
+    assert rel(dmod, Pr["blocks.0.modulation"].grad) < 3e-2
+    assert rel(dctx.float(), cr.grad) < 3e-2, rel(dctx.float(), cr.grad)
+    for n, gr in G.items():
+        r = rel(gr, Pr["blocks.0." + n].grad)
+        if n.endswith(("k.bias", "k_img.bias")):   # shift-invariant directions: near-zero grads
+            w = Pr["blocks.0." + n[:-4] + "weight"].grad
+            assert (gr.cpu() - Pr["blocks.0." + n].grad).norm() < 3e-2 * w.norm(), n
+        else:
+            assert r < 3e-2, (n, r)
+
+
+@pytest.mark.parametrize("tag", ["t2v", "i2v"])
+def test_real_width_block_vs_reference(golden, tag):
+    """14B block (C=5120, 40 heads, F=13824), L=48, against the reference's own outputs."""
+    g = golden("real_block_" + tag)
+    i2v = tag == "i2v"
+    P = seeded_params(block_shapes("blocks.0.", 5120, 13824, i2v))
+    L, Lc = 48, (512 if not i2v else 769)
+    x = torch.from_numpy(seeded.randn("blk.x", (1, L, 5120)))
+    e = torch.from_numpy(seeded.randn("blk.e", (1, 6, 5120), 0.1))
+    ctx = torch.from_numpy(seeded.randn("blk.ctx" + tag, (1, Lc, 5120))).to(torch.bfloat16)
+    up = torch.from_numpy(seeded.randn("blk.up" + tag, (1, L, 5120)))
+    out, dx, de, dmod, dctx, G = run_block(P, x, e, ctx, tuple(g["grid"][0]), L, 40, i2v, up)
+    assert rel(out, g["out"]) < 1e-2, rel(out, g["out"])
+    assert rel(dx, g["dx"]) < 3e-2, rel(dx, g["dx"])
+    assert rel(de, g["de"]) < 3e-2, rel(de, g["de"])
+    assert abs(dctx.double().norm().item() / float(g["dctx_norm"]) - 1) < 3e-2
+    for k, v in g.items():
+        if k.startswith("gnorm/") and not k.endswith("modulation"):
+            n = k[6:]
+            gn = G[n].double().norm().item()
+            assert abs(gn / float(v) - 1) < 3e-2, (n, gn, float(v))
+            gp = (G[n].double().cpu().flatten() * torch.from_numpy(
+                seeded.randn("proj:" + n, (G[n].numel(),))).double()).sum().item()
+            assert abs(gp - float(g["gproj/" + n])) < 5e-2 * float(v), (n, gp, float(g["gproj/" + n]))

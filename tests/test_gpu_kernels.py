@@ -1,0 +1,208 @@
+"""Per-kernel parity on the MI355X: HIP C-ABI kernels vs the CPU oracle / fp32 references.
+
+Tolerances (bf16 operands, fp32 accumulate): GEMM rel-L2 <= 2e-3 vs an fp32 GEMM of the same
+bf16 operands (bf16 output rounding is 2^-9); attention / norms rel-L2 <= 5e-3 fwd, 2e-2 bwd
+(SURVEY.md §8c tolerances).
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import wan_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from prfl_amd import ops as _ops
+    return _ops
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 384, 192), (105, 512, 256),
+                                   (1000, 640, 144), (48, 15360, 5120)])
+def test_gemm_forward_epilogues(ops, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    a = bf(torch.randn(M, K, generator=g)).to(DEV)
+    w = bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    bias = bf(torch.randn(N, generator=g) * 0.1).to(DEV)
+    ref = a.float() @ w.float().t() + bias.float()
+    out = ops.linear(a, w, bias)
+    assert rel(out, ref) < 3e-3
+    # GELU epilogue with pre-activation store
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    act = ops.linear(a, w, bias, ops.EPI_GELU, aux=pre)
+    assert rel(pre, ref) < 3e-3
+    assert rel(act, torch.nn.functional.gelu(pre.float(), approximate="tanh")) < 3e-3
+    # gated fp32 residual: res + bf16(acc+b)*gate
+    res = torch.randn(M, N, generator=g).to(DEV)
+    gate = (torch.randn(N, generator=g) * 0.5).to(DEV)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    o = ops.linear(a, w, bias, ops.EPI_RESID, gate=gate, res=res, aux=y)
+    assert rel(o, res + ref * gate) < 3e-3
+    assert torch.equal(o, res + y.float() * gate)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (105, 256, 296), (1000, 136, 520)])
+def test_gemm_backward_layouts(ops, M, N, K):
+    """dX = dY W (N-major B) and dW = dY^T X (both MN-major): the ds_read_b64_tr_b16 paths."""
+    g = torch.Generator().manual_seed(N)
+    dy = bf(torch.randn(M, N, generator=g)).to(DEV)
+    w = bf(torch.randn(N, K, generator=g)).to(DEV)
+    x = bf(torch.randn(M, K, generator=g)).to(DEV)
+    dx = ops.linear_dx(dy, w)
+    assert rel(dx, dy.float() @ w.float()) < 3e-3
+    dw = ops.linear_dw(dy, x)
+    assert rel(dw, dy.float().t() @ x.float()) < 1e-4
+    ops.linear_dw(dy, x, out=dw, accumulate=True)
+    assert rel(dw, 2 * (dy.float().t() @ x.float())) < 1e-4
+    pre = bf(torch.randn(M, K, generator=g)).to(DEV)
+    dg = ops.linear_dx(dy, w, epilogue=ops.EPI_DGELU, aux=pre)
+    p = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(p, approximate="tanh").backward(bf(dy.float() @ w.float()).float())
+    assert rel(dg, p.grad) < 5e-3
+
+
+def test_gemm_identity_asymmetric(ops):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 128
+    a = torch.eye(n, dtype=torch.bfloat16, device=DEV)
+    b = bf(torch.arange(n * n, dtype=torch.float32).view(n, n) % 97).to(DEV)
+    out = ops.linear(a, b)
+    assert torch.equal(out.float(), b.float().t())
+
+
+@pytest.mark.parametrize("Lq,Lk,H,klen", [(128, 128, 1, 128), (200, 333, 2, 333), (105, 512, 2, 20),
+                                          (1000, 1000, 3, 937)])
+def test_attention_fwd_bwd(ops, Lq, Lk, H, klen):
+    g = torch.Generator().manual_seed(Lq + Lk)
+    C = H * 128
+    q = bf(torch.randn(Lq, C, generator=g) * 1.5)
+    k = bf(torch.randn(Lk, C, generator=g) * 1.5)
+    v = bf(torch.randn(Lk, C, generator=g))
+    o, lse = ops.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), H, k_len=klen)
+    qr = q.float().view(1, Lq, H, 128).requires_grad_(True)
+    kr = k.float().view(1, Lk, H, 128).requires_grad_(True)
+    vr = v.float().view(1, Lk, H, 128).requires_grad_(True)
+    ref = O.attention(qr, kr, vr, k_len=klen if klen < Lk else None)
+    assert rel(o, ref.reshape(Lq, C)) < 5e-3
+    do = bf(torch.randn(Lq, C, generator=g))
+    ref.backward(do.float().view(1, Lq, H, 128))
+    dq, dk, dv = ops.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), o, do.to(DEV), lse, H, k_len=klen)
+    assert rel(dq, qr.grad.reshape(Lq, C)) < 2e-2
+    assert rel(dk, kr.grad.reshape(Lk, C)) < 2e-2
+    assert rel(dv, vr.grad.reshape(Lk, C)) < 2e-2
+    if klen < Lk:
+        assert dk[klen:].abs().max().item() == 0 and dv[klen:].abs().max().item() == 0
+
+
+def test_attention_rescale_spike(ops):
+    """Force the online-softmax rescale: one key gets a huge score in a late tile (rule 26)."""
+    L, C = 256, 128
+    g = torch.Generator().manual_seed(3)
+    q = torch.randn(L, C, generator=g) * 0.1
+    k = torch.randn(L, C, generator=g) * 0.1
+    k[200] = q[5] * 60.0
+    q, k = bf(q), bf(k)
+    v = bf(torch.randn(L, C, generator=g))
+    o, _ = ops.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), 1)
+    ref = O.attention(q.float().view(1, L, 1, C), k.float().view(1, L, 1, C), v.float().view(1, L, 1, C))
+    assert rel(o, ref.reshape(L, C)) < 5e-3
+
+
+@pytest.mark.parametrize("C,x_bf16,affine", [(256, False, False), (256, True, False),
+                                             (5120, False, False), (5120, False, True)])
+def test_ln_mod(ops, C, x_bf16, affine):
+    L = 77
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(L, C, generator=g) * 2 + 0.3
+    if x_bf16:
+        x = bf(x)
+    sc = torch.randn(C, generator=g) * 0.1
+    sh = torch.randn(C, generator=g) * 0.1
+    w = 1 + torch.randn(C, generator=g) * 0.1
+    bb = torch.randn(C, generator=g) * 0.1
+    xr = x.float().requires_grad_(True)
+    scr, shr = sc.clone().requires_grad_(True), sh.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), bb.clone().requires_grad_(True)
+    if affine:
+        ref = O.layer_norm(xr, 1e-6, wr, br)
+        out, mean, rstd = ops.ln_mod_fwd(x.to(DEV), w=w.to(DEV), b=bb.to(DEV))
+    else:
+        ref = O.layer_norm(xr, 1e-6, in_bf16=x_bf16) * (1 + scr) + shr
+        out, mean, rstd = ops.ln_mod_fwd(x.to(DEV), scale=sc.to(DEV), shift=sh.to(DEV))
+    assert rel(out, O.bf(ref)) < 3e-3
+    dy = bf(torch.randn(L, C, generator=g))
+    ref.backward(dy.float())
+    dx = torch.zeros(L, C, device=DEV)
+    if affine:
+        d0, d1 = ops.ln_mod_bwd(dy.to(DEV), x.to(DEV), mean, rstd, dx, w=w.to(DEV))
+        assert rel(d0, wr.grad) < 5e-3 and rel(d1, br.grad) < 5e-3
+    else:
+        d0, d1 = ops.ln_mod_bwd(dy.to(DEV), x.to(DEV), mean, rstd, dx, scale=sc.to(DEV))
+        assert rel(d0, scr.grad) < 5e-3 and rel(d1, shr.grad) < 5e-3
+    assert rel(dx, xr.grad) < 5e-3
+
+
+@pytest.mark.parametrize("rope", [True, False])
+def test_rms_rope(ops, rope):
+    C, H = 256, 2
+    grid = (3, 5, 7)
+    L = 112   # 105 rotated + 7 pass-through rows
+    g = torch.Generator().manual_seed(11)
+    x = bf(torch.randn(L, C, generator=g) * 3)
+    w = 1 + torch.randn(C, generator=g) * 0.1
+    freqs = O.rope_freqs(128)
+    tab = ops.rope_table(freqs, DEV) if rope else None
+    out, rstd = ops.rms_rope_fwd(x.to(DEV), w.to(DEV), 1e-6, tab, grid if rope else (0, 0, 0))
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    n = O.rms_norm(xr, wr)
+    if rope:
+        n = O.rope_apply(n.view(1, L, H, 128), torch.tensor([grid]), freqs).view(L, C)
+    assert rel(out, O.bf(n)) < 3e-3
+    do = bf(torch.randn(L, C, generator=g))
+    n.backward(do.float())
+    dx, dw = ops.rms_rope_bwd(do.to(DEV), x.to(DEV), rstd, w.to(DEV), tab,
+                              grid if rope else (0, 0, 0))
+    assert rel(dx, xr.grad) < 1e-2
+    assert rel(dw, wr.grad) < 5e-3
+
+
+def test_adamw_matches_torch(ops):
+    g = torch.Generator().manual_seed(5)
+    p = torch.randn(10007, generator=g)
+    grads = [torch.randn(10007, generator=g) for _ in range(3)]
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=5e-6, betas=(0.9, 0.999), weight_decay=0.01, eps=1e-8,
+                            foreach=False)
+    pd, m, v = p.to(DEV), torch.zeros(10007, device=DEV), torch.zeros(10007, device=DEV)
+    for step, gr in enumerate(grads, 1):
+        ref.grad = gr.clone()
+        opt.step()
+        ops.adamw_(pd, gr.to(DEV), m, v, 5e-6, 0.9, 0.999, 1e-8, 0.01, step)
+    assert (pd.cpu() - ref.detach()).abs().max().item() < 1e-6
+
+
+def test_sumsq_scale(ops):
+    x = torch.randn(100003, device=DEV)
+    out = torch.zeros(1, device=DEV)
+    ops.sumsq_(x, out)
+    assert abs(out.item() / (x.double() ** 2).sum().item() - 1) < 1e-4
+    f = torch.tensor([0.5], device=DEV)
+    y = x.clone()
+    ops.scale_(y, f)
+    assert torch.equal(y, x * 0.5)
