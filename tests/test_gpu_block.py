@@ -93,7 +93,15 @@ def test_real_width_block_vs_reference(golden, tag):
         if k.startswith("gnorm/") and not k.endswith("modulation"):
             n = k[6:]
             gn = G[n].double().norm().item()
-            assert abs(gn / float(v) - 1) < 3e-2, (n, gn, float(v))
             gp = (G[n].double().cpu().flatten() * torch.from_numpy(
                 seeded.randn("proj:" + n, (G[n].numel(),))).double()).sum().item()
+            if n.endswith(("k.bias", "k_img.bias")):
+                # softmax shift-invariance makes these near-zero by cancellation: judge the
+                # error against the matching weight gradient's scale
+                scale = float(g["gnorm/" + n[:-4] + "weight"])
+                assert abs(gn - float(v)) < 3e-2 * scale, (n, gn, float(v))
+                assert abs(gp - float(g["gproj/" + n])) < 5e-2 * scale, n
+                continue
+            assert abs(gn / float(v) - 1) < 3e-2, (n, gn, float(v))
             assert abs(gp - float(g["gproj/" + n])) < 5e-2 * float(v), (n, gp, float(g["gproj/" + n]))
+    assert abs(dmod.double().norm().item() / float(g["gnorm/modulation"]) - 1) < 3e-2
