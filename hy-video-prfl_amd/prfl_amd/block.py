@@ -133,9 +133,10 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
     return out, S
 
 
-def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
+def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     """Backward of block_forward_one.  dout fp32 [L, C] (consumed/overwritten).  Parameter
-    gradients are accumulated into the fp32 dict G; returns (dx fp32, de [6, C], dctx fp32)."""
+    gradients are accumulated into the fp32 dict G (skipped entirely when want_w is False, e.g.
+    for the frozen reward-model trunk); returns (dx fp32, de [6, C], dctx fp32)."""
     g = P.__getitem__
     L, C = x.shape
     nh, eps = meta.num_heads, meta.eps
@@ -143,12 +144,16 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
     de = [None] * 6
 
     def acc(name, val):
+        if not want_w:
+            return
         if G.get(name) is None:
             G[name] = val
         else:
             G[name].add_(val)
 
     def dw(name, dy, xin):
+        if not want_w:
+            return
         if G.get(name) is None:
             G[name] = ops.linear_dw(dy, xin)
         else:
@@ -162,7 +167,8 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
     dfpre = ops.linear_dx(dy2, W.w2, epilogue=EPI_DGELU, aux=S["fpre"])
     del dy2
     dw("ffn.0.weight", dfpre, S["h2"])
-    acc("ffn.0.bias", ops.colsum(dfpre))
+    if want_w:
+        acc("ffn.0.bias", ops.colsum(dfpre))
     dh2 = ops.linear_dx(dfpre, W.w1)
     del dfpre
     de[4], de[3] = ops.ln_mod_bwd(dh2, S["x2"], S["m2"], S["r2"], dx, scale=e[4])
@@ -181,7 +187,8 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
     dqc_raw, dnq = ops.rms_rope_bwd(dqc, S["qc_raw"], S["rqc"], g("cross_attn.norm_q.weight"))
     acc("cross_attn.norm_q.weight", dnq)
     dw("cross_attn.q.weight", dqc_raw, S["n3"])
-    acc("cross_attn.q.bias", ops.colsum(dqc_raw))
+    if want_w:
+        acc("cross_attn.q.bias", ops.colsum(dqc_raw))
     dn3 = ops.linear_dx(dqc_raw, W.wcq)
     dw3, db3 = ops.ln_mod_bwd(dn3, S["x1"], S["m3"], S["r3"], dx, w=g("norm3.weight"))
     acc("norm3.weight", dw3)
@@ -190,9 +197,11 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
     dkc_raw, dnk = ops.rms_rope_bwd(dkc, S["kc_raw"], S["rkc"], g("cross_attn.norm_k.weight"))
     acc("cross_attn.norm_k.weight", dnk)
     dw("cross_attn.k.weight", dkc_raw, ctx_t)
-    acc("cross_attn.k.bias", ops.colsum(dkc_raw))
+    if want_w:
+        acc("cross_attn.k.bias", ops.colsum(dkc_raw))
     dw("cross_attn.v.weight", dvc, ctx_t)
-    acc("cross_attn.v.bias", ops.colsum(dvc))
+    if want_w:
+        acc("cross_attn.v.bias", ops.colsum(dvc))
     dctx = torch.empty(ctx.shape, dtype=torch.float32, device=x.device)
     n_img = ctx.shape[0] - ctx_t.shape[0]
     dctx_t = dctx[n_img:]
@@ -203,9 +212,11 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
                                          g("cross_attn.norm_k_img.weight"))
         acc("cross_attn.norm_k_img.weight", dnki)
         dw("cross_attn.k_img.weight", dki_raw, ctx_i)
-        acc("cross_attn.k_img.bias", ops.colsum(dki_raw))
+        if want_w:
+            acc("cross_attn.k_img.bias", ops.colsum(dki_raw))
         dw("cross_attn.v_img.weight", dvi, ctx_i)
-        acc("cross_attn.v_img.bias", ops.colsum(dvi))
+        if want_w:
+            acc("cross_attn.v_img.bias", ops.colsum(dvi))
         dctx_i = dctx[:n_img]
         ops.gemm(dki_raw, W.wck_img, dctx_i, n_img, C, C, True, False, ops.EPI_F32)
         ops.gemm(dvi, W.wcv_img, dctx_i, n_img, C, C, True, False, ops.EPI_F32, accumulate=True)
@@ -229,7 +240,7 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G):
     del dqr, dkr
     for i, n in enumerate("qkv"):
         dw(f"self_attn.{n}.weight", dqkv[:, i * C:(i + 1) * C], S["h1"])
-    dbqkv = ops.colsum(dqkv)
+    dbqkv = ops.colsum(dqkv) if want_w else None
     for i, n in enumerate("qkv"):
         acc(f"self_attn.{n}.bias", dbqkv[i * C:(i + 1) * C].clone())
     dh1 = ops.gemm(dqkv, W.wqkv, torch.empty(L, C, dtype=BF16, device=x.device), L, C, 3 * C,
@@ -266,7 +277,8 @@ class WanBlockFn(torch.autograd.Function):
         for b in range(x.shape[0]):
             _, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=True)
             d = dout[b].to(torch.float32).contiguous().clone()
-            dx, de, dc = block_backward_one(P, W, x[b], e[b], context[b], meta, b, S, d, G)
+            dx, de, dc = block_backward_one(P, W, x[b], e[b], context[b], meta, b, S, d, G,
+                                            want_w=any(fctx.needs_input_grad[5:]))
             del S
             dxs.append(dx)
             des.append(de)
