@@ -1,0 +1,219 @@
+"""PRFL training-step benchmark (BASELINE.json metric) on 1..8 MI355X, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload prfl_t2v_480|pavrm_t2v_480]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (default): `configs/train_prfl_t2v_480.yaml` on one GPU per rank — the full PRFL
+iteration (flow-matching SFT step + reward step: 19-step no-grad UniPC rollout, grad-enabled
+generator step, differentiable UniPC step, 8-block latent reward model + QueryAttention + MLP,
+backward through all of it, clip, AdamW every 5th micro-step) on the 14B Wan2.1 T2V DiT
+(40 blocks, C=5120) at 480p x 81f (latent [16,21,60,104] -> L = 32760 tokens), random-init
+weights (head perturbed so gradients are non-zero), synthetic latents/text.  The 720p x 81f
+metric config does not fit a single 288 GB replica with fp32 AdamW state, so this
+is the largest single-GPU configuration in BASELINE.json `configs`.
+
+Multi-GPU: pure data parallel (weak scaling, one sample per rank), RCCL all-reduce of the
+generator gradients overlapped with the backward (prfl_amd/dist.py).  `value` = PRFL sample-
+iterations completed by all ranks per second.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hy-video-prfl_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+C, F, NH, NL, TXT = 5120, 13824, 40, 40, 512
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def block_fwd_flops(L, Lctx=TXT):
+    """8LC^2 + 4L^2C + 4LC^2 + 4 Lctx C^2 + 4 L Lctx C + 4LCF."""
+    return 8 * L * C * C + 4 * L * L * C + 4 * L * C * C + 4 * Lctx * C * C + 4 * L * Lctx * C + 4 * L * C * F
+
+
+def iteration_flops(L, mid):
+    """Algorithmic FLOPs of one PRFL iteration (no recompute): SFT 3G + reward (mid+1)G+2G+3R."""
+    G = NL * block_fwd_flops(L)
+    R = 8 * block_fwd_flops(L)
+    return 3 * G + (mid + 1) * G + 2 * G + 3 * R
+
+
+def setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def build_models(dev, seed):
+    from prfl_amd.model import WanModel
+    from prfl_amd.network import MLP, QueryAttention
+    torch.manual_seed(seed)
+    with torch.device(dev):
+        gen = WanModel(model_type="t2v", dim=C, ffn_dim=F, freq_dim=256, text_dim=4096, out_dim=16,
+                       num_heads=NH, num_layers=NL, in_dim=16)
+        torch.nn.init.normal_(gen.head.head.weight, std=0.02)   # random-init trap
+        lrm = WanModel(model_type="t2v", dim=C, ffn_dim=F, freq_dim=256, text_dim=4096, out_dim=16,
+                       num_heads=NH, num_layers=8, in_dim=16)    # == blocks[0:8] of the base model
+        del lrm.head
+        lrm.head = None
+        qa = QueryAttention(C, 1, 8, 0., return_type="query")
+        mlp = MLP(C)
+    for p in list(lrm.parameters()) + list(qa.parameters()) + list(mlp.parameters()):
+        p.requires_grad_(False)
+    return gen, lrm, qa, mlp
+
+
+def cpu_baseline(L_sample=4096):
+    """The oracle (fp32 CPU restatement) timed on this host: one real-width 14B block forward +
+    backward at L_sample tokens; extrapolated by algorithmic FLOPs to one PRFL iteration."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from oracle import wan_oracle as O
+    from shapes import block_shapes
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    P = {n: (torch.randn(s, generator=g) / math.sqrt(s[-1] if len(s) > 1 else 1) * (0.02 if len(s) == 1 else 1))
+         .requires_grad_(True) for n, s in block_shapes("b.", C, F)}
+    for n in P:
+        if "norm" in n and n.endswith("weight"):
+            P[n] = (1 + P[n].detach()).requires_grad_(True)
+    f, h, w = 1, 64, L_sample // 64
+    x = torch.randn(1, L_sample, C, generator=g).requires_grad_(True)
+    e = torch.randn(1, 6, C, generator=g) * 0.1
+    ctx = torch.randn(1, TXT, C, generator=g).to(torch.bfloat16).float()
+    t0 = time.time()
+    out = O.block_forward(P, "b.", x, e, torch.tensor([[f, h, w]]), O.rope_freqs(128), ctx, NH,
+                          seq_len=L_sample)
+    out.sum().backward()
+    dt = time.time() - t0
+    flops = 3 * block_fwd_flops(L_sample)
+    return dt, flops, threads
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="prfl_t2v_480", choices=["prfl_t2v_480", "pavrm_t2v_480"])
+    ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world, rank, local = setup()
+    dev = torch.device("cuda", local)
+    from prfl_amd import ops
+    from prfl_amd.train import PAVRMTrainer, PRFLTrainer
+
+    Fl, Hl, Wl = 21, 60, 104                         # 480p x 81f latent (gen_wanx_latent.py:117-149)
+    L = Fl * (Hl // 2) * (Wl // 2)
+    gen, lrm, qa, mlp = build_models(dev, 110221)
+    g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
+    latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
+    text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
+    if args.workload == "prfl_t2v_480":
+        tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0)
+
+        def one(step):
+            a = tr.sft_step(step, latents, text, L, generator=g)
+            b = tr.reward_step(step, latents, text, L, mid_timestep=args.mid, generator=g)
+            return a, b
+        flops_it = iteration_flops(L, args.mid)
+    else:
+        del gen
+        for blk in lrm.blocks:
+            blk.requires_grad_(True)
+        tr = PAVRMTrainer(lrm, qa, mlp)
+        label = torch.ones(1, device=dev)
+
+        def one(step):
+            return tr.step(latents, text, L, label, generator=g), None
+        flops_it = 3 * 8 * block_fwd_flops(L)
+
+    # step indices: the timed window ends on an optimizer-step iteration ((step+1) % 5 == 0)
+    first = max(0, (5 - (args.warmup + args.steps) % 5) % 5)
+    for s in range(first, first + args.warmup):
+        one(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.reset_peak_memory_stats()
+    ops.prof_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.time()
+    for s in range(first + args.warmup, first + args.warmup + args.steps):
+        last = one(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.time() - t0
+    ops.prof_enable(False)
+    prof = ops.prof_collect()
+    peak_alloc = torch.cuda.max_memory_allocated() / 1e9
+    peak_res = torch.cuda.max_memory_reserved() / 1e9
+    tmax = torch.tensor([dt, peak_res], device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt, peak_res = tmax.tolist()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # dominant kernel by time over the timed region
+    kinds = {k: v for k, v in prof.items() if v["count"] and k in ("gemm", "attn_fwd", "attn_bwd_dkdv",
+                                                                   "attn_bwd_dq")}
+    dom = max(kinds, key=lambda k: kinds[k]["ms"])
+    d = kinds[dom]
+    achieved = d["work"] / (d["ms"] * 1e-3) / 1e12
+    value = world * args.steps / dt
+    res = {
+        "metric": "PRFL train steps/sec (whole node) + peak HBM GB, 14B DiT",
+        "value": round(value, 6), "unit": "PRFL iterations/s (all ranks)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents/text, random-init 14B weights",
+        "config": {"workload": ("train_prfl_t2v_480: SFT + reward step, mid_timestep=%d" % args.mid
+                                if args.workload == "prfl_t2v_480" else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
+                   "model": "Wan2.1-T2V-14B (40 blocks, C=5120)", "latent": [16, Fl, Hl, Wl],
+                   "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
+        "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),
+        "algorithmic_tflop_per_step": round(flops_it / 1e12, 1),
+        "achieved_tflops_per_gpu": round(flops_it * args.steps / dt / 1e12, 1),
+        "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 1),
+                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "launches": d["count"], "avg_launch_ms": round(d["ms"] / d["count"], 3),
+                     "work_per_launch_tflop": round(d["work"] / d["count"] / 1e12, 3),
+                     "traffic": None},
+        "kernels": {k: {"count": v["count"], "ms": round(v["ms"], 1),
+                        "rate": round(v["work"] / (v["ms"] * 1e-3) / (1e9 if k in ("ln", "rms", "eltwise", "adamw") else 1e12), 1)}
+                    for k, v in prof.items() if v["count"]},
+    }
+    if not args.no_cpu_baseline:
+        cdt, cfl, thr = cpu_baseline()
+        cpu_rate = cfl / cdt
+        res["cpu_baseline"] = {"value": flops_it and cpu_rate / flops_it, "unit": "PRFL iterations/s",
+                               "cores": thr, "kind": "port",
+                               "sample": f"oracle fp32 14B block fwd+bwd at L=4096 on host: {cdt:.1f} s "
+                                         f"({cpu_rate/1e12:.2f} TFLOP/s), extrapolated by FLOPs to one "
+                                         f"iteration ({flops_it/1e15:.1f} PFLOP)"}
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

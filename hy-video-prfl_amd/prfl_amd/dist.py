@@ -1,0 +1,111 @@
+"""Data-parallel gradient exchange for the PRFL step (replaces FSDP FULL_SHARD + Ulysses SP of
+`fsdp_utils.py:66-122` / `communication.py:40-160` with pure batch DP over RCCL/xGMI).
+
+Every rank holds a full replica (288 GB HBM fits the 14B fp32 master + AdamW state at 480p).
+The reference reduces the FRESH gradient of every backward (FSDP reduce-scatters each micro-step,
+no `no_sync`) and accumulates the reduced gradient; `GradReducer` does the same:
+
+  before backward : stash accumulated grads, clear .grad
+  during backward : a post-accumulate-grad hook fires per parameter as soon as its block's fused
+                    backward node returns (reverse layer order) and launches an async all-reduce
+                    on RCCL's stream -> communication overlaps the remaining blocks' backward
+  after backward  : wait, average (gloo has no AVG), add the stash back
+
+Block gradients are 105-283 MB tensors, well past the point where a ring all-reduce is
+bandwidth-bound on xGMI, so tensors are reduced individually (no flatten/copy buckets); the
+small 1-D tensors (biases, norm weights) of a block are coalesced into one flat reduce.
+"""
+import torch
+import torch.distributed as dist
+
+
+def is_dist():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+class GradReducer:
+    def __init__(self, params, small_numel=1 << 16):
+        self.params = [p for p in params if p.requires_grad]
+        self.world = dist.get_world_size() if is_dist() else 1
+        self.small_numel = small_numel
+        self.works = []
+        self.stash = {}
+        self.small_pending = []
+        self.backend = dist.get_backend() if is_dist() else None
+        self.handles = []
+        if self.world > 1:
+            for p in self.params:
+                self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _op(self):
+        return dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+
+    def _hook(self, p):
+        if p.numel() <= self.small_numel:
+            self.small_pending.append(p)
+            if sum(q.numel() for q in self.small_pending) >= 8 * self.small_numel:
+                self._flush_small()
+            return
+        self.works.append((dist.all_reduce(p.grad, op=self._op(), async_op=True), [p.grad]))
+
+    def _flush_small(self):
+        if not self.small_pending:
+            return
+        ps, self.small_pending = self.small_pending, []
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        w = dist.all_reduce(flat, op=self._op(), async_op=True)
+        self.works.append((w, (flat, ps)))
+
+    def begin(self):
+        """Call before loss.backward()."""
+        for p in self.params:
+            if p.grad is not None:
+                self.stash[p] = p.grad
+                p.grad = None
+
+    def end(self):
+        """Call after loss.backward(): completes the exchange and re-accumulates."""
+        if self.world > 1:
+            self._flush_small()
+            for w, payload in self.works:
+                w.wait()
+                if isinstance(payload, tuple):
+                    flat, ps = payload
+                    if self.backend != "nccl":
+                        flat.div_(self.world)
+                    off = 0
+                    for p in ps:
+                        n = p.numel()
+                        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                        off += n
+                elif self.backend != "nccl":
+                    payload[0].div_(self.world)
+            self.works = []
+        for p, g in self.stash.items():
+            if p.grad is None:
+                p.grad = g
+            else:
+                g.add_(p.grad)
+                p.grad = g
+        self.stash = {}
+
+
+def broadcast_int(v, src=0, device="cpu"):
+    """`train_prfl.py:640-652`: rank 0 draws mid_timestep, every rank uses it."""
+    if not is_dist():
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.long, device=device)
+    dist.broadcast(t, src=src)
+    return int(t.item())
+
+
+def all_reduce_mean(t):
+    if not is_dist():
+        return t
+    t = t.clone()
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, dist.ReduceOp.AVG)
+    else:
+        dist.all_reduce(t, dist.ReduceOp.SUM)
+        t /= dist.get_world_size()
+    return t

@@ -125,9 +125,8 @@ class FlowUniPCMultistepScheduler:
             raise ValueError("call set_timesteps first")
         if self._step_index is None:
             self._init_step_index(timestep)
-        dev = sample.device
-        if self.sigmas.device != dev:
-            self.sigmas = self.sigmas.to(dev)
+        # sigmas stay on the host as 0-dim fp32 scalars (as in the reference): scalar x device
+        # tensor keeps the sample dtype and needs no host<->device traffic
         i = self._step_index
         m_t = sample - self.sigmas[i] * model_output                # convert_model_output (:321)
         if i > 0 and (i - 1) not in self.disable_corrector and self.last_sample is not None:

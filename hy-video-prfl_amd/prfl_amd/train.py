@@ -1,0 +1,178 @@
+"""PRFL / PAVRM training steps on the MI355X path.
+
+Restates the per-iteration logic of the reference drivers (which cannot travel to the GPU box):
+  * ``sft_step``     — `scripts/prfl/train_prfl.py:900-1034` (flow-matching SFT loss)
+  * ``reward_step``  — `scripts/prfl/train_prfl.py:585-898`  (no-grad UniPC rollout to a random
+                       mid timestep, one grad-enabled generator step, one differentiable UniPC
+                       step, frozen latent reward model + QueryAttention + MLP, hinge loss)
+  * ``pavrm_step``   — `scripts/pavrm/train_pavrm.py:671-920` (BCE reward-model training)
+  * ``build_lrm``    — `train_prfl.py:217-266` (first `trainable_blocks` of a Wan model, no head)
+Optimizer semantics kept: loss / gradient_accumulation_steps, clip_grad_norm_(1.0) on the
+accumulated grads every micro-step, optimizer.step() when (step+1) % accum == 0 in BOTH steps.
+"""
+import random
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .dist import GradReducer, all_reduce_mean, broadcast_int
+from .network import forward_mlp
+from .optim import AdamW, clip_grad_norm_
+from .schedulers import FlowMatchDiscreteScheduler, FlowUniPCMultistepScheduler
+
+
+def batch2list(batch):
+    return [item for item in batch]
+
+
+def list2batch(lst):
+    return torch.stack(lst)
+
+
+def build_lrm(model, trainable_blocks=range(8)):
+    """Latent reward model trunk: keep blocks[trainable_blocks], drop the head, freeze all
+    (the reference leaves requires_grad=True on the kept blocks but never optimises them)."""
+    keep = set(trainable_blocks)
+    model.blocks = nn.ModuleList([b for i, b in enumerate(model.blocks) if i in keep])
+    if hasattr(model, "head"):
+        del model.head
+        model.head = None
+    for p in model.parameters():
+        p.requires_grad_(False)
+    return model
+
+
+class PRFLTrainer:
+    def __init__(self, transformer, lrm, query_attention, mlp, lr=5e-6, weight_decay=0.01,
+                 grad_accum=5.0, flow_shift=5.0, inference_steps=40, feature_layer=(8,),
+                 max_grad_norm=1.0):
+        self.transformer, self.lrm, self.qa, self.mlp = transformer, lrm, query_attention, mlp
+        params = [p for p in transformer.parameters() if p.requires_grad]
+        self.params = params
+        self.optimizer = AdamW(params, lr=lr, weight_decay=weight_decay)
+        self.reducer = GradReducer(params)
+        self.grad_accum = grad_accum
+        self.inference_steps = inference_steps
+        self.feature_layer = list(feature_layer)
+        self.max_grad_norm = max_grad_norm
+        self.flow_shift = flow_shift
+        self.fm = FlowMatchDiscreteScheduler(shift=flow_shift)
+        self.fm.set_timesteps(1000, dtype=torch.int64)
+        self.unipc = FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                                 use_dynamic_shifting=False)
+
+    def _backward_and_step(self, loss, step):
+        self.reducer.begin()
+        loss.backward()
+        self.reducer.end()
+        grad_norm = clip_grad_norm_(self.params, self.max_grad_norm)
+        if (step + 1) % self.grad_accum == 0:
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+        return grad_norm
+
+    def _kw(self, latent, text_states, seq_len, image_embeds, cond):
+        return dict(context=batch2list(text_states), seq_len=seq_len, clip_fea=image_embeds,
+                    y=batch2list(cond) if cond is not None else None)
+
+    def sft_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
+                 generator=None):
+        """train_prfl.py:900-980."""
+        bsz = latents.shape[0]
+        noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                            device=latents.device)
+        timestep, sigma = self.fm.get_train_timestep_and_sigma(
+            weighting_scheme="uniform", batch_size=bsz, device=latents.device, n_dim=latents.ndim)
+        noisy = self.fm.add_noise(latents, noise, sigma)
+        pred = list2batch(self.transformer(x=batch2list(noisy), t=timestep,
+                                           **self._kw(noisy, text_states, seq_len, image_embeds,
+                                                      cond)))
+        target = self.fm.get_train_target(latents, noise)
+        loss = torch.mean((pred.float() - target.float()) ** 2) / self.grad_accum
+        grad_norm = self._backward_and_step(loss, step)
+        return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm)
+
+    def reward_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
+                    mid_timestep=None, generator=None):
+        """train_prfl.py:585-846."""
+        sch = self.unipc
+        sch.set_timesteps(num_inference_steps=self.inference_steps, device=latents.device,
+                          shift=self.flow_shift)
+        timesteps = sch.timesteps
+        latent = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                             device=latents.device)
+        if mid_timestep is None:
+            mid_timestep = random.randint(0, self.inference_steps - 2)
+        mid = broadcast_int(mid_timestep, device=latents.device)
+        kw = self._kw(latent, text_states, seq_len, image_embeds, cond)
+        dev = latents.device
+        with torch.no_grad():                                          # :665-699
+            for i in range(mid):
+                t = timesteps[i]
+                pred = list2batch(self.transformer(x=batch2list(latent), t=t.reshape(1),
+                                                   **kw))
+                latent = sch.step(pred, t, latent, return_dict=False)[0]
+        t_mid = timesteps[mid]                                         # :708-735
+        pred = list2batch(self.transformer(x=batch2list(latent), t=t_mid.reshape(1),
+                                           **kw))
+        latent = sch.step(pred, t_mid, latent, return_dict=False)[0]
+        t1 = timesteps[mid + 1]                                        # :745-798
+        feats = list2batch(self.lrm(x=batch2list(latent), t=t1.reshape(1),
+                                    output_features=True, selected_layers=self.feature_layer,
+                                    **kw))
+        reward = forward_mlp(self.mlp, self.qa(feats))
+        loss = 0.1 * F.relu(-reward.squeeze() + 2).mean()
+        loss = loss / self.grad_accum
+        grad_norm = self._backward_and_step(loss, step)
+        return dict(loss=all_reduce_mean(loss.detach().float()), grad_norm=grad_norm, mid=mid,
+                    reward=reward.detach())
+
+
+class PAVRMTrainer:
+    """train_pavrm.py:671-920 with loss 'ce': BCE(sigmoid(MLP(QA(features))), label)."""
+
+    def __init__(self, lrm, query_attention, mlp, lr=1e-6, lr_head=1e-5, weight_decay=0.01,
+                 flow_shift=5.0, feature_layer=(8,)):
+        self.lrm, self.qa, self.mlp = lrm, query_attention, mlp
+        for p in lrm.parameters():
+            p.requires_grad_(False)
+        for blk in lrm.blocks:                       # trainable blocks (train_pavrm.py:215-235)
+            for p in blk.parameters():
+                p.requires_grad_(True)
+        for m in (query_attention, mlp):
+            for p in m.parameters():
+                p.requires_grad_(True)
+        self.trunk_params = [p for p in lrm.parameters() if p.requires_grad]
+        self.head_params = list(query_attention.parameters()) + list(mlp.parameters())
+        self.opt_trunk = AdamW(self.trunk_params, lr=lr, weight_decay=weight_decay)
+        self.opt_head = AdamW(self.head_params, lr=lr_head, weight_decay=weight_decay)
+        self.reducer = GradReducer(self.trunk_params + self.head_params)
+        self.fm = FlowMatchDiscreteScheduler(shift=flow_shift)
+        self.fm.set_timesteps(1000, dtype=torch.int64)
+        self.feature_layer = list(feature_layer)
+
+    def step(self, latents, text_states, seq_len, label, image_embeds=None, cond=None,
+             generator=None):
+        bsz = latents.shape[0]
+        noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                            device=latents.device)
+        timestep, sigma = self.fm.get_train_timestep_and_sigma(
+            weighting_scheme="uniform", batch_size=bsz, device=latents.device, n_dim=latents.ndim)
+        noisy = self.fm.add_noise(latents, noise, sigma)
+        feats = list2batch(self.lrm(x=batch2list(noisy), t=timestep, context=batch2list(text_states),
+                                    seq_len=seq_len, clip_fea=image_embeds,
+                                    y=batch2list(cond) if cond is not None else None,
+                                    output_features=True, selected_layers=self.feature_layer))
+        out = forward_mlp(self.mlp, self.qa(feats))
+        loss = F.binary_cross_entropy(out.squeeze().float(), label.squeeze().float())
+        self.reducer.begin()
+        loss.backward()
+        self.reducer.end()
+        grad_norm = clip_grad_norm_(self.trunk_params, 1.0)
+        clip_grad_norm_(self.head_params, 1.0)
+        self.opt_trunk.step()
+        self.opt_head.step()
+        self.opt_trunk.zero_grad()
+        self.opt_head.zero_grad()
+        return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm)

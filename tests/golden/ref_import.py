@@ -12,8 +12,9 @@ What is substituted, and why none of it changes arithmetic:
   diffusers does and otherwise are plain ``nn.Module``/``object``.
 * ``easydict``/``ftfy`` are imported by non-hot-path config modules; stubbed as dict/identity.
 * ``flash_attn`` (third-party, `requirements.txt:16`, README pins 2.5.0) is absent.  Its
-  published algorithm — softmax(q·kᵀ·d^-½)·v with bf16 inputs, fp32 softmax, keys ≥ k_len
-  masked, bf16 output — is restated by ``sdpa_flash_attention`` and swapped in at the reference
+  published FA2 algorithm — forward softmax(q·kᵀ·d^-½)·v with bf16 inputs, fp32 softmax, P
+  rounded to bf16 for P·V, keys ≥ k_len masked, bf16 output; backward with D = rowsum(dO∘O) taken
+  from the bf16 output — is restated by ``sdpa_flash_attention`` and swapped in at the reference
   call site ``model.flash_attention`` (`attention.py:24-130`).
 * The reference wraps fp32 islands in ``torch.cuda.amp.autocast(dtype=torch.float32)``
   (`model.py:339,347,354,386,590`) and disables autocast for RoPE (`model.py:35,60`).  On a CPU
@@ -115,28 +116,53 @@ class _AmpShim:
         return torch.autocast("cpu", dtype=dtype, enabled=enabled)
 
 
+class _FlashAttnRestated(torch.autograd.Function):
+    """flash_attn (FA2) published algorithm on [B, L, N, D] fp32 copies of bf16 q/k/v:
+    forward  P = exp(s - rowmax) (bf16 for the P.V product), l = sum of fp32 P, O = bf16(P.V / l)
+    backward dV = P^T dO, dP = dO V^T, D = rowsum(dO * O) with the bf16 O, dS = P (dP - D),
+             dQ = scale dS K, dK = scale dS^T Q   (FA2 paper Alg. 2; flash_attn/flash_bwd_*)"""
+
+    @staticmethod
+    def forward(ctx, q, k, v, k_len, scale):
+        bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+        qb, kb, vb = bf(q), bf(k), bf(v)
+        s = torch.einsum("blnd,bmnd->bnlm", qb, kb) * scale
+        if k_len is not None:
+            lk = k.shape[1]
+            mask = torch.arange(lk).view(1, 1, 1, lk) >= k_len.view(-1, 1, 1, 1).to(torch.long)
+            s = s.masked_fill(mask, float("-inf"))
+        m = s.amax(-1, keepdim=True)
+        p = torch.exp(s - m)
+        l = p.sum(-1, keepdim=True)
+        o = bf(torch.einsum("bnlm,bmnd->blnd", bf(p), vb) / l.permute(0, 2, 1, 3))
+        ctx.save_for_backward(qb, kb, vb, o, p / l)
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qb, kb, vb, o, P = ctx.saved_tensors
+        do = do.to(torch.bfloat16).float()
+        dv = torch.einsum("bnlm,blnd->bmnd", P, do)
+        dp = torch.einsum("blnd,bmnd->bnlm", do, vb)
+        delta = (do * o).sum(-1).permute(0, 2, 1).unsqueeze(-1)
+        ds = P * (dp - delta)
+        dq = torch.einsum("bnlm,bmnd->blnd", ds, kb) * ctx.scale
+        dk = torch.einsum("bnlm,blnd->bmnd", ds, qb) * ctx.scale
+        return dq, dk, dv, None, None
+
+
 def sdpa_flash_attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=None,
                          q_scale=None, causal=False, window_size=(-1, -1), deterministic=False,
                          dtype=torch.bfloat16, version=None):
     """Restatement of flash_attn varlen semantics used at `attention.py:96-127`."""
+    assert not causal and dropout_p == 0 and q_lens is None
     out_dtype = q.dtype
-    b, lq, lk = q.size(0), q.size(1), k.size(1)
     with torch.autocast("cpu", enabled=False):
-        qb = q.to(dtype).float()
-        kb = k.to(dtype).float()
-        vb = v.to(dtype).float()
         if q_scale is not None:
-            qb = qb * q_scale
-        scale = softmax_scale if softmax_scale is not None else qb.size(-1) ** -0.5
-        s = torch.einsum("blnd,bmnd->bnlm", qb, kb) * scale
-        if k_lens is not None:
-            mask = torch.arange(lk).view(1, 1, 1, lk) >= k_lens.view(b, 1, 1, 1).to(torch.long)
-            s = s.masked_fill(mask, float("-inf"))
-        p = torch.softmax(s, dim=-1)
-        o = torch.einsum("bnlm,bmnd->blnd", p, vb)
-        if q_lens is not None:
-            qmask = torch.arange(lq).view(1, lq, 1, 1) >= q_lens.view(b, 1, 1, 1).to(torch.long)
-            o = o.masked_fill(qmask, 0.0)
+            q = q * q_scale
+        scale = softmax_scale if softmax_scale is not None else q.size(-1) ** -0.5
+        o = _FlashAttnRestated.apply(q.float(), k.float(), v.float(), k_lens, scale)
     return o.to(dtype).to(out_dtype)
 
 

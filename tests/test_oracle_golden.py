@@ -9,6 +9,7 @@ import torch
 
 import seeded
 from shapes import TOY, block_shapes, model_shapes, qa_shapes, mlp_shapes, seeded_params
+from tolerance import key_path_scale
 from oracle import wan_oracle as O
 
 torch.set_num_threads(8)
@@ -64,12 +65,9 @@ def test_toy_model_fwd_bwd(golden, model_type):
         if k.startswith("grad/"):
             n = k[5:]
             r = rel(P[n].grad, v)
-            if n.endswith(("k.bias", "k_img.bias")):
-                # softmax is shift-invariant in keys, so these grads are near-zero by
-                # cancellation; judge the error against the matching weight grad's scale
-                wn = n[:-4] + "weight"
-                scale = np.linalg.norm(g["grad/" + wn]) if "grad/" + wn in g else float(g["gnorm/" + wn])
-                assert (P[n].grad.flatten() - torch.from_numpy(v)).norm().item() < 2e-2 * scale, n
+            scale = key_path_scale(g, n)
+            if scale is not None:
+                assert (P[n].grad.flatten() - torch.from_numpy(v)).norm().item() < 3e-2 * scale, n
             else:
                 assert r < 3e-2, (n, r)
             checked += 1
