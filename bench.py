@@ -145,7 +145,11 @@ def main():
     # step indices: the timed window ends on an optimizer-step iteration ((step+1) % 5 == 0)
     first = max(0, (5 - (args.warmup + args.steps) % 5) % 5)
     for s in range(first, first + args.warmup):
+        t_w = time.time()
         one(s)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup iteration {s}: {time.time() - t_w:.1f} s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -240,9 +240,10 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     del dqr, dkr
     for i, n in enumerate("qkv"):
         dw(f"self_attn.{n}.weight", dqkv[:, i * C:(i + 1) * C], S["h1"])
-    dbqkv = ops.colsum(dqkv) if want_w else None
-    for i, n in enumerate("qkv"):
-        acc(f"self_attn.{n}.bias", dbqkv[i * C:(i + 1) * C].clone())
+    if want_w:
+        dbqkv = ops.colsum(dqkv)
+        for i, n in enumerate("qkv"):
+            acc(f"self_attn.{n}.bias", dbqkv[i * C:(i + 1) * C].clone())
     dh1 = ops.gemm(dqkv, W.wqkv, torch.empty(L, C, dtype=BF16, device=x.device), L, C, 3 * C,
                    True, False, EPI_BF16)
     del dqkv
