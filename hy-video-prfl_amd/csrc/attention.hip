@@ -81,6 +81,9 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
 }
 
 // ============================================================================ forward ====
+// SHORT_KV: separate instantiation for the 512/257-key cross-attention so profiles separate it
+// from the self-attention (same code today).
+template <bool SHORT_KV>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 128;
@@ -463,7 +466,10 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  if (kid == KID_ATTN_FWD)
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();
