@@ -15,6 +15,8 @@
 // Backward (FA2 recomputation, no atomics): delta = rowsum(dO*O); a dK/dV kernel owns 128 keys
 // per workgroup (32 per wave, accumulators resident) and sweeps all query tiles; a dQ kernel owns
 // 128 queries and sweeps all key tiles.  Both reuse the same lane mappings as the forward.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -216,6 +218,156 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       *(bf16x4*)(Ob + (int64_t)qr * a.ldo + dt * 16 + 4 * g) = v;
     }
     if (g == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m[sub] + log2f(l[sub]);
+  }
+}
+
+// ===================================================================== forward (32x32) ====
+// 8 waves x 32 queries = 256 queries per workgroup; K/V tiles of 64 keys register-staged into a
+// 2-deep LDS ring shared by all 8 waves.  MFMA 32x32x16 (8 of its 32 issue cycles hold the SIMD's
+// vector issue, vs 8 of 16 for 16x16x32), so the softmax VALU hides under the matrix pipe.
+//   S^T[key][q] = K . Q^T  : A = K rows (ds_read_b128), B = Q^T fragments kept in registers
+//   lane (q = l&31, h = l>>5) holds keys (r&3) + 8(r>>2) + 4h of a 32-key tile in acc r
+//   P packed to bf16 straight from the accumulator (k order 16s + 8(j>>2) + 4h + (j&3)) is the
+//   B operand of O^T[d][q] += V^T . P^T, with V^T fragments read by ds_read_b64_tr_b16 in the
+//   same permuted key order.  Row max is exchanged between the two lane halves once per tile;
+//   row sums stay per-half until the end; O is rescaled only when some row max grew (exact).
+template <bool SHORT_KV>
+__global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+
+  bf16x8 qf[8];
+  {
+    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = NEG_INF, lsum = 0.f;
+
+  const int nkv = (a.k_len + 63) / 64;
+  u32x4 rk[2], rv[2];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
+      const int key = min(t * 64 + row, a.Lk - 1);
+      rk[i] = *(const u32x4*)(Kb + (int64_t)key * a.ldk + ch * 8);
+      rv[i] = *(const u32x4*)(Vb + (int64_t)key * a.ldv + ch * 8);
+    }
+  };
+  auto sstore = [&](int st) {
+    char* Ks = smem + st * 32768;
+    char* Vs = Ks + 16384;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
+      *(u32x4*)(Ks + off16(row, ch)) = rk[i];
+      *(u32x4*)(Vs + offT(row, ch << 4)) = rv[i];
+    }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  for (int t = 0; t < nkv; ++t) {
+    const char* Ks = smem + (t & 1) * 32768;
+    const char* Vs = Ks + 16384;
+    if (t + 1 < nkv) gload(t + 1);
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
+      const int row = kt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + off16(row, ks * 2 + hh));
+        s[kt] = mfma32(kf, qf[ks], s[kt]);
+      }
+    }
+    const int kbase = t * 64;
+    if (kbase + 64 > a.k_len) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
+    }
+    float mx = NEG_INF;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx * a.sl2);
+    if (__any(mnew > m)) {                      // rescale only when a row max grew
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+      m = mnew;
+    }
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(s[kt][r] * a.sl2 - m);
+        s[kt][r] = p;
+        lsum += p;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
+                              f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
+                              f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
+                              f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+    }
+    // O^T[d][q] += V^T P^T ; V^T fragment: lane group g reads keys base + 4*(g>>1) + {0..3},
+    // base + 8 + 4*(g>>1) + {0..3}, columns d0 = dt*32 + 16*(g&1)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const int rb = ra + 8;
+          const bf16x8 vf = cat8(lds_read_tr(Vs + offT(ra, byte)), lds_read_tr(Vs + offT(rb, byte)));
+          o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
+        }
+    }
+    if (t + 1 < nkv) sstore((t + 1) & 1);
+    __syncthreads();
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  const int qr = q0 + w * 32 + l32;
+  if (qr < a.Lq) {
+    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
+    const float inv = 1.f / lsum;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * inv);
+        *(bf16x4*)(Ob + dt * 32 + 8 * rg + 4 * hh) = v;
+      }
+    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m + log2f(lsum);
   }
 }
 
@@ -466,10 +618,17 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
-  if (kid == KID_ATTN_FWD)
+  static const int impl = getenv("PRFL_ATTN_FWD16") ? 16 : 32;
+  if (impl == 32) {
+    if (kid == KID_ATTN_FWD)
+      hipLaunchKernelGGL(attn_fwd32_kernel<false>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL(attn_fwd32_kernel<true>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
+  } else if (kid == KID_ATTN_FWD) {
     hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  }
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();

@@ -16,6 +16,8 @@
 // written to the other LDS buffer after the MFMAs (one barrier per K step).
 // The MFMA is issued as D = B.A^T so each lane owns 4 consecutive n of one row m: epilogue stores
 // are 8-16 B contiguous per lane.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -119,6 +121,71 @@ __device__ __forceinline__ void tile_coords(int bid, int M, int N, int& tm, int&
 }
 
 template <bool A_KC, bool B_KC, int EPI>
+__device__ __forceinline__ void epilogue_tile(const GemmArgs& g, f32x4 v, int m, int n) {
+#pragma clang diagnostic push
+      if (EPI == EPI_F32) {
+        float* cp = (float*)g.C + (int64_t)m * g.ldc + n;
+        if (g.accumulate) {
+          f32x4 o = *(f32x4*)cp;
+          v = v + o;
+        }
+        *(f32x4*)cp = v;
+        return;
+      }
+      if (EPI == EPI_DGELU) {
+        const bf16x4 pre = *(const bf16x4*)(g.aux + (int64_t)m * g.ldaux + n);
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(bf2f(pre[r])));
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+        return;
+      }
+      float y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + (g.bias ? bf2f(g.bias[n + r]) : 0.f));
+      if (EPI == EPI_BF16) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+      } else if (EPI == EPI_GELU) {
+        bf16x4 o, pre;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pre[r] = f2bf(y[r]);
+          o[r] = f2bf(gelu_tanh(y[r]));
+        }
+        if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
+        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+      } else if (EPI == EPI_RESID) {
+        if (g.aux) {
+          bf16x4 yo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
+          *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
+        }
+        float rv[4];
+        if (g.res_bf16) {
+          const bf16x4 rr = *(const bf16x4*)((const bf16*)g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = bf2f(rr[r]);
+        } else {
+          const f32x4 rr = *(const f32x4*)((const float*)g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = rr[r];
+        }
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = g.gate ? g.gate[n + r] : 1.f;
+          o[r] = rv[r] + mul_rn(y[r], gt);  // x + y*e (two roundings, as in torch)
+        }
+        *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
+      }
+#pragma clang diagnostic pop
+}
+
+template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   // stage st: A at smem + st*2*TILE_BYTES, B right after it
@@ -181,74 +248,155 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
       if (n >= g.N) continue;
-      f32x4 v = acc[i][j];
-      if (EPI == EPI_F32) {
-        float* cp = (float*)g.C + (int64_t)m * g.ldc + n;
-        if (g.accumulate) {
-          f32x4 o = *(f32x4*)cp;
-          v = v + o;
-        }
-        *(f32x4*)cp = v;
-        continue;
+      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
+    }
+  }
+}
+
+// =========================================================================== 256x256 tile ===
+// 8 waves (2 along M x 4 along N), each 128x64 = 8x4 MFMA 16x16x32 tiles; BK = 64; operands
+// land in LDS by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece per wave instruction) into a
+// 2-deep ring (2 x 64 KiB).  Tile t+1 stays in flight across the barriers while tile t computes
+// (counted `s_waitcnt vmcnt(8)` + raw s_barrier; no __syncthreads in the loop, one __shared__
+// array), per MI355X guide §5 "Pipelining across barriers".  The LDS images are the same
+// swizzled layouts as above, produced by permuting each lane's SOURCE address (the DMA
+// destination is lane-linear).  Requires K % 64 == 0 and MN-major extents % 256 == 0.
+constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
+constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
+
+__device__ __forceinline__ int swz_mn(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+template <bool KC>
+__device__ __forceinline__ void dma_tile(char* lds, const bf16* __restrict__ P, int64_t ld, int rows,
+                                         int r0, int k0, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wid * 4 + i;                     // 32 pieces of 1 KiB
+    const bf16* src;
+    if (KC) {          // piece = 8 rows x 128 B; lane -> (row, physical chunk)
+      const int row = piece * 8 + (lane >> 3), pc = lane & 7;
+      const int gr = min(r0 + row, rows - 1);
+      src = P + (int64_t)gr * ld + k0 + ((pc ^ (row & 7)) << 3);
+    } else {           // piece = 2 k-rows x 512 B
+      const int kr = piece * 2 + (lane >> 5), pb = (lane & 31) << 4;
+      const int lb = pb ^ (swz_mn(kr) << 5);
+      src = P + (int64_t)(k0 + kr) * ld + r0 + (lb >> 1);
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag2(const char* lds, int base, int s, int lane) {
+  if (KC) {
+    const int row = base + (lane & 15);
+    const int kc = s * 4 + (lane >> 4);
+    return *(const bf16x8*)(lds + row * 128 + ((kc ^ (row & 7)) << 4));
+  } else {
+    const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+    const int col = (base + 4 * p) * 2;
+    const int k0 = s * 32 + g * 8 + q, k1 = k0 + 4;
+    bf16x4 lo = lds_read_tr(lds + k0 * 512 + (col ^ (swz_mn(k0) << 5)));
+    bf16x4 hi = lds_read_tr(lds + k1 * 512 + (col ^ (swz_mn(k1) << 5)));
+    return cat8(lo, hi);
+  }
+}
+
+__device__ __forceinline__ void tile_coords2(int bid, int M, int N, int& tm, int& tn) {
+  const int ntm = (M + BM2 - 1) / BM2, ntn = (N + BN2 - 1) / BN2;
+  const int nwg = ntm * ntn;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int GM = 4;
+  const int group = w / (GM * ntn);
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  const int within = w - group * GM * ntn;
+  tm = first_m + within % gsz;
+  tn = within / gsz;
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A|B]
+  int tm, tn;
+  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  dma_tile<A_KC>(smem, g.A, g.lda, g.M, m0, 0, wid, lane);
+  dma_tile<B_KC>(smem + TILE2, g.B, g.ldb, g.N, n0, 0, wid, lane);
+  if (nk > 1) {
+    dma_tile<A_KC>(smem + 2 * TILE2, g.A, g.lda, g.M, m0, BK, wid, lane);
+    dma_tile<B_KC>(smem + 3 * TILE2, g.B, g.ldb, g.N, n0, BK, wid, lane);
+  }
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed (8 DMA instructions per wave per tile; tile t+1 may stay in flight)
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* As = smem + (t & 1) * 2 * TILE2;
+    const char* Bs = As + TILE2;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = read_frag2<B_KC>(Bs, wc * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 af = read_frag2<A_KC>(As, wr * 128 + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bf[j], af, acc[i][j]);
       }
-      if (EPI == EPI_DGELU) {
-        const bf16x4 pre = *(const bf16x4*)(g.aux + (int64_t)m * g.ldaux + n);
-        bf16x4 o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                     // every wave is done reading stage t&1
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) {
+      char* st = smem + (t & 1) * 2 * TILE2;
+      dma_tile<A_KC>(st, g.A, g.lda, g.M, m0, (t + 2) * BK, wid, lane);
+      dma_tile<B_KC>(st + TILE2, g.B, g.ldb, g.N, n0, (t + 2) * BK, wid, lane);
+    }
+  }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(bf2f(pre[r])));
-        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-        continue;
-      }
-      float y[4];
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + (g.bias ? bf2f(g.bias[n + r]) : 0.f));
-      if (EPI == EPI_BF16) {
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
-        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-      } else if (EPI == EPI_GELU) {
-        bf16x4 o, pre;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pre[r] = f2bf(y[r]);
-          o[r] = f2bf(gelu_tanh(y[r]));
-        }
-        if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
-        *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-      } else if (EPI == EPI_RESID) {
-        if (g.aux) {
-          bf16x4 yo;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
-          *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
-        }
-        float rv[4];
-        if (g.res_bf16) {
-          const bf16x4 rr = *(const bf16x4*)((const bf16*)g.res + (int64_t)m * g.ldr + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rv[r] = bf2f(rr[r]);
-        } else {
-          const f32x4 rr = *(const f32x4*)((const float*)g.res + (int64_t)m * g.ldr + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rv[r] = rr[r];
-        }
-        f32x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gt = g.gate ? g.gate[n + r] : 1.f;
-          o[r] = rv[r] + mul_rn(y[r], gt);  // x + y*e (two roundings, as in torch)
-        }
-        *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
     }
   }
 }
 
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s) {
-  const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);
+  static const bool no256 = getenv("PRFL_GEMM128") != nullptr;
+  const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
+  const bool ok256 = !no256 && (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) &&
+                     (B_KC || g.N % BN2 == 0) && nt256 >= 96;
+  if (ok256) {
+    hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
+  } else {
+    const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);
+  }
   PRFL_LAUNCH_CHECK();
   return 0;
 }
@@ -274,6 +422,28 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_GEMM, s);
   int rc = (int)hipErrorInvalidValue;
+  // weight gradients with a token count K that is not a multiple of 64: the bulk of K goes
+  // through the 256-tile kernel, the < 64-row tail is accumulated by a second (128-tile) launch
+  if (epilogue == EPI_F32 && !a_kmajor && !b_kmajor && (K % BK) != 0 && K > BK &&
+      (M % BM2) == 0 && (N % BN2) == 0) {
+    const int64_t Kmain = K - K % BK;
+    GemmArgs gm = g;
+    gm.K = (int)Kmain;
+    rc = launch<false, false, EPI_F32>(gm, s);
+    if (rc == 0) {
+      GemmArgs gt = g;
+      gt.A = g.A + Kmain * lda;
+      gt.B = g.B + Kmain * ldb;
+      gt.K = (int)(K - Kmain);
+      gt.accumulate = 1;
+      const int ntm = (gt.M + BM - 1) / BM, ntn = (gt.N + BN - 1) / BN;
+      hipLaunchKernelGGL((gemm_kernel<false, false, EPI_F32>), dim3(ntm * ntn), dim3(NT), 0, s, gt);
+      rc = (int)hipGetLastError();
+    }
+    prfl_prof::set_work(2.0 * (double)M * (double)N * (double)K);
+    prfl_prof::end(KID_GEMM, s);
+    return rc;
+  }
 #define GEMM_CASE(AK, BK_, E) \
   if (a_kmajor == AK && b_kmajor == BK_ && epilogue == E) rc = launch<AK, BK_, E>(g, s);
   GEMM_CASE(1, 1, EPI_BF16)

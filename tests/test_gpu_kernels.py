@@ -33,7 +33,8 @@ def bf(t):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 384, 192), (105, 512, 256),
-                                   (1000, 640, 144), (48, 15360, 5120)])
+                                   (1000, 640, 144), (48, 15360, 5120), (2300, 3072, 512),
+                                   (4096, 5120, 1024)])
 def test_gemm_forward_epilogues(ops, M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N)
     a = bf(torch.randn(M, K, generator=g)).to(DEV)
@@ -56,7 +57,8 @@ def test_gemm_forward_epilogues(ops, M, N, K):
     assert torch.equal(o, res + y.float() * gate)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (105, 256, 296), (1000, 136, 520)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (105, 256, 296), (1000, 136, 520),
+                                   (3072, 2048, 3072), (3000, 2048, 3072)])
 def test_gemm_backward_layouts(ops, M, N, K):
     """dX = dY W (N-major B) and dW = dY^T X (both MN-major): the ds_read_b64_tr_b16 paths."""
     g = torch.Generator().manual_seed(N)
