@@ -1,0 +1,42 @@
+"""Dev probe: isolated hot kernels at the 480p x 81f shapes (L = 32760, C = 5120, 40 heads),
+for rocprofv3 counter runs.  usage: python tools/prof_kernels.py [attn|gemm|attn_bwd] [reps]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hy-video-prfl_amd")]
+import torch  # noqa: E402
+from prfl_amd import ops  # noqa: E402
+
+which = sys.argv[1] if len(sys.argv) > 1 else "attn"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+L, C, NH, F = 32760, 5120, 40, 13824
+dev = "cuda"
+g = torch.Generator(device=dev).manual_seed(0)
+if which in ("attn", "attn_bwd"):
+    qkv = torch.randn(L, 3 * C, device=dev, generator=g).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    o, lse = ops.attn_fwd(q, k, v, NH)
+    do = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
+    fl = 4 * L * L * C
+    for i in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        if which == "attn":
+            ops.attn_fwd(q, k, v, NH, out=o)
+        else:
+            ops.attn_bwd(q, k, v, o, do, lse, NH)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        print(f"{which} {dt*1e3:.2f} ms  {fl*(1 if which=='attn' else 2.5)/dt/1e12:.0f} TF/s", flush=True)
+else:
+    x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(F, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    for i in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        y = ops.linear(x, w)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        print(f"gemm {L}x{F}x{C} {dt*1e3:.2f} ms  {2*L*F*C/dt/1e12:.0f} TF/s", flush=True)
