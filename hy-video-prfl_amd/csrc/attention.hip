@@ -600,6 +600,241 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
 }
 
+// ================================================================== backward (32x32) ======
+// Same lane geometry as attn_fwd32: MFMA 32x32x16, accumulators consumed in place as the next
+// product's B operand, transposed operands from ds_read_b64_tr_b16.
+//
+// dQ: 8 waves x 32 queries; per 64-key tile S^T = K.Q^T, dP^T = V.dO^T (query on the lane, so
+// LSE and D are per-lane scalars), dS^T = P^T (dP^T - D) packed to bf16, dQ^T += K^T dS^T.
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq32_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[32768];  // K tile (image B) | V tile
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
+    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
+  }
+  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
+  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
+  f32x16 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+  char* Ks = smem;
+  char* Vs = smem + 16384;
+  const int nkv = (a.k_len + 63) / 64;
+  u32x4 rk[2], rv[2];
+  auto fetch = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
+      const int kr = min(kb + row, a.Lk - 1);
+      rk[i] = *(const u32x4*)(Kb + (int64_t)kr * a.ldk + ch * 8);
+      rv[i] = *(const u32x4*)(Vb + (int64_t)kr * a.ldv + ch * 8);
+    }
+  };
+  fetch(0);
+  for (int t = 0; t < nkv; ++t) {
+    const int kb = t * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
+      *(u32x4*)(Ks + offB(row, ch << 4)) = rk[i];
+      *(u32x4*)(Vs + off16(row, ch)) = rv[i];
+    }
+    __syncthreads();
+    if (t + 1 < nkv) fetch(kb + 64);
+    bf16x8 dsp[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+      const int row = kt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
+        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
+        dpt[r] = p * (dpt[r] - del);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
+          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
+        }
+    }
+    __syncthreads();
+  }
+  const int qo = q0 + w * 32 + l32;
+  if (qo < a.Lq) {
+    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
+        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
+      }
+  }
+}
+
+// dK, dV: 4 waves x 32 keys (K, V fragments and dK^T, dV^T accumulators resident, one wave per
+// SIMD); sweeps query tiles of 64 (two 32-query halves).  S = Q.K^T and dP = dO.V^T with the key
+// on the lane, so P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv32_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[32768 + 512];  // Q | dO (image B) | LSE, D
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
+  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
+  const int key = k0 + w * 32 + l32;
+  const bool kvalid = key < a.k_len;
+  const int kr = min(key, a.Lk - 1);
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    kf[ks] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ks * 16 + hh * 8);
+    vf[ks] = *(const bf16x8*)(Vb + (int64_t)kr * a.ldv + ks * 16 + hh * 8);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  char* Qs = smem;
+  char* Ds = smem + 16384;
+  float* Ls = (float*)(smem + 32768);   // [64] LSE (+inf past Lq), then [64] D
+  const int nq = (a.Lq + 63) / 64;
+  u32x4 rq[4], rd[4];
+  float rl = 0.f;
+  auto fetch = [&](int qb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      const int q = min(qb + row, a.Lq - 1);
+      rq[i] = *(const u32x4*)(Qb + (int64_t)q * a.ldq + ch * 8);
+      rd[i] = *(const u32x4*)(dOb + (int64_t)q * a.lddo + ch * 8);
+    }
+    if (tid < 128) {
+      const int q = qb + (tid & 63);
+      rl = tid < 64 ? (q < a.Lq ? lseb[q] : __builtin_huge_valf()) : (q < a.Lq ? delb[q] : 0.f);
+    }
+  };
+  fetch(0);
+  for (int t = 0; t < nq; ++t) {
+    const int qb = t * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
+      *(u32x4*)(Qs + offB(row, ch << 4)) = rq[i];
+      *(u32x4*)(Ds + offB(row, ch << 4)) = rd[i];
+    }
+    if (tid < 128) Ls[tid] = rl;
+    __syncthreads();
+    if (t + 1 < nq) fetch(qb + 64);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+      const int row = qt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        st = mfma32(*(const bf16x8*)(Qs + offB(row, (ks * 2 + hh) * 16)), kf[ks], st);
+        dpt = mfma32(*(const bf16x8*)(Ds + offB(row, (ks * 2 + hh) * 16)), vf[ks], dpt);
+      }
+      // rows q = qb + qt*32 + (r&3) + 8(r>>2) + 4hh
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int q4 = qt * 32 + 8 * rg + 4 * hh;
+        const f32x4 l4 = *(const f32x4*)(Ls + q4);
+        const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = kvalid ? __builtin_amdgcn_exp2f(st[rg * 4 + r] * a.sl2 - l4[r]) : 0.f;
+          st[rg * 4 + r] = p;
+          dpt[rg * 4 + r] = p * (dpt[rg * 4 + r] - d4[r]);
+        }
+      }
+      bf16x8 pk[2], dk8[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pk[s2] = (bf16x8){f2bf(st[8 * s2 + 0]), f2bf(st[8 * s2 + 1]), f2bf(st[8 * s2 + 2]),
+                          f2bf(st[8 * s2 + 3]), f2bf(st[8 * s2 + 4]), f2bf(st[8 * s2 + 5]),
+                          f2bf(st[8 * s2 + 6]), f2bf(st[8 * s2 + 7])};
+        dk8[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                           f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                           f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = qt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const bf16x8 dof = cat8(lds_read_tr(Ds + offB(ra, byte)), lds_read_tr(Ds + offB(ra + 8, byte)));
+          const bf16x8 qtf = cat8(lds_read_tr(Qs + offB(ra, byte)), lds_read_tr(Qs + offB(ra + 8, byte)));
+          dv[dt] = mfma32(dof, pk[s2], dv[dt]);
+          dk[dt] = mfma32(qtf, dk8[s2], dk[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (key < a.Lk) {
+    bf16* dKb = a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk;
+    bf16* dVb = a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 vk, vv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vk[r] = f2bf(dk[dt][rg * 4 + r] * a.scale);
+          vv[r] = f2bf(dv[dt][rg * 4 + r]);
+        }
+        *(bf16x4*)(dKb + dt * 32 + 8 * rg + 4 * hh) = vk;
+        *(bf16x4*)(dVb + dt * 32 + 8 * rg + 4 * hh) = vv;
+      }
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
@@ -655,13 +890,20 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
                 scale * 1.4426950408889634f, scale};
+  static const bool bwd16 = getenv("PRFL_ATTN_BWD16") != nullptr;
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
+  if (bwd16)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv32_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();
   prfl_prof::begin(KID_ATTN_BWD_DQ, s);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  if (bwd16)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq32_kernel, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
   PRFL_LAUNCH_CHECK();

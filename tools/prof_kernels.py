@@ -30,6 +30,13 @@ if which in ("attn", "attn_bwd"):
         torch.cuda.synchronize()
         dt = time.time() - t0
         print(f"{which} {dt*1e3:.2f} ms  {fl*(1 if which=='attn' else 2.5)/dt/1e12:.0f} TF/s", flush=True)
+    ops.prof_enable(True)
+    ops.attn_fwd(q, k, v, NH, out=o) if which == "attn" else ops.attn_bwd(q, k, v, o, do, lse, NH)
+    torch.cuda.synchronize()
+    ops.prof_enable(False)
+    for kname, d in ops.prof_collect().items():
+        if d["count"]:
+            print(f"  {kname}: {d['ms']:.2f} ms  {d['work'] / (d['ms'] * 1e-3) / 1e12:.0f} TF/s", flush=True)
 else:
     x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(F, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
