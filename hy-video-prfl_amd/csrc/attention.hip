@@ -31,6 +31,7 @@ struct AttnArgs {
   float* LSE;            // [B][H][Lq], log2 domain
   int Lq, Lk, H, k_len;
   float sl2;             // softmax_scale * log2(e)
+  int stagger;           // attn_fwd32: waves 4-7 run one phase behind waves 0-3
 };
 
 struct AttnBwdArgs {
@@ -233,10 +234,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 //   row sums stay per-half until the end; O is rescaled only when some row max grew (exact).
 template <bool SHORT_KV>
 __global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  __shared__ __attribute__((aligned(16))) char smem[3 * 32768];
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
+  // Waves 4-7 share SIMDs with waves 0-3 and run one phase behind them: they apply tile t-1's
+  // P.V after tile t's S, so one partner's softmax VALU overlaps the other's MFMA work instead
+  // of both partners reaching it together between the same barriers.  Per-wave arithmetic and
+  // its order are unchanged (bit-identical output).  Needs a 3-stage K/V ring.
+  const bool late = a.stagger && w >= 4;
   const bf16* Qb = a.Q + b * a.bq + h * HD;
   const bf16* Kb = a.K + b * a.bk + h * HD;
   const bf16* Vb = a.V + b * a.bv + h * HD;
@@ -273,18 +279,37 @@ __global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
       *(u32x4*)(Ks + off16(row, ch)) = rk[i];
-      *(u32x4*)(Vs + offT(row, ch << 4)) = rv[i];
+      *(u32x4*)(Vs + offB(row, ch << 4)) = rv[i];
+    }
+  };
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  bf16x8 pf[2][2];
+  // O^T[d][q] += V^T P^T ; V^T fragment: lane group g reads keys base + 4*(g>>1) + {0..3},
+  // base + 8 + 4*(g>>1) + {0..3}, columns d0 = dt*32 + 16*(g&1)
+  auto pv = [&](const char* Vs) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const int rb = ra + 8;
+          const bf16x8 vf = cat8(lds_read_tr(Vs + offB(ra, byte)), lds_read_tr(Vs + offB(rb, byte)));
+          o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
+        }
     }
   };
   gload(0);
   sstore(0);
   __syncthreads();
 
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  int st = 0, st_prev = 0;
   for (int t = 0; t < nkv; ++t) {
-    const char* Ks = smem + (t & 1) * 32768;
-    const char* Vs = Ks + 16384;
+    const char* Ks = smem + st * 32768;
     if (t + 1 < nkv) gload(t + 1);
+    if (late && t > 0) pv(smem + st_prev * 32768 + 16384);
     f32x16 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -319,7 +344,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
       m = mnew;
     }
-    bf16x8 pf[2][2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
@@ -335,24 +359,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
                               f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
                               f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
     }
-    // O^T[d][q] += V^T P^T ; V^T fragment: lane group g reads keys base + 4*(g>>1) + {0..3},
-    // base + 8 + 4*(g>>1) + {0..3}, columns d0 = dt*32 + 16*(g&1)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const int rb = ra + 8;
-          const bf16x8 vf = cat8(lds_read_tr(Vs + offT(ra, byte)), lds_read_tr(Vs + offT(rb, byte)));
-          o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
-        }
-    }
-    if (t + 1 < nkv) sstore((t + 1) & 1);
+    if (!late) pv(Ks + 16384);
+    st_prev = st;
+    st = st == 2 ? 0 : st + 1;
+    if (t + 1 < nkv) sstore(st);
     __syncthreads();
   }
+  if (late) pv(smem + st_prev * 32768 + 16384);
   lsum += __shfl_xor(lsum, 32, 64);
   const int qr = q0 + w * 32 + l32;
   if (qr < a.Lq) {
@@ -849,7 +862,7 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
     return (int)hipErrorInvalidValue;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f};
+             scale * 1.4426950408889634f, getenv("PRFL_ATTN_NOSTAGGER") ? 0 : 1};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);

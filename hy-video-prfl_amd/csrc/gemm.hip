@@ -10,7 +10,7 @@
 //
 // Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16x32 tiles.
 // K-contiguous tiles live in LDS as [128 rows][64 k] (128-B rows, 16-B chunk XOR row&7) and feed
-// ds_read_b128; MN-contiguous tiles live as [64 k][128] (256-B rows, 32-B XOR (k&7)<<5) and feed
+// ds_read_b128; MN-contiguous tiles live as [64 k][128] (256-B rows, 32-B XOR swz_mn(k)) and feed
 // ds_read_b64_tr_b16 (hardware transpose), so both layouts reach the same MFMA fragment.
 // Global->LDS staging is register double-buffered: tile t+1 is loaded while tile t computes and is
 // written to the other LDS buffer after the MFMAs (one barrier per K step).
@@ -39,6 +39,10 @@ struct GemmArgs {
   bf16* aux; int64_t ldaux;  // GELU: pre-activation out; RESID: y out; DGELU: pre-activation in
   int accumulate;       // EPI_F32: C += acc
 };
+
+// 32-B granule swizzle of MN-major rows: k bits {0,1,3} -> the 8 k-rows one ds_read_b64_tr_b16
+// lane group touches (q = k&3, g&1 = k>>3 bit) land on 8 different granules (conflict-free)
+__device__ __forceinline__ int swz_mn(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 // ---- staging: global -> registers -----------------------------------------------------------
 template <bool KC>
@@ -79,7 +83,7 @@ __device__ __forceinline__ void store_tile(char* lds, const u32x4 (&r)[4]) {
       off = row * 128 + ((kc ^ (row & 7)) << 4);
     } else {
       const int kr = c >> 4, mc = c & 15;
-      off = kr * 256 + ((mc << 4) ^ ((kr & 7) << 5));
+      off = kr * 256 + ((mc << 4) ^ (swz_mn(kr) << 5));
     }
     *(u32x4*)(lds + off) = r[i];
   }
@@ -97,8 +101,8 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int s, in
     const int col = (base + 4 * p) * 2;
     const int k0 = s * 32 + g * 8 + q;
     const int k1 = k0 + 4;
-    bf16x4 lo = lds_read_tr(lds + k0 * 256 + (col ^ ((k0 & 7) << 5)));
-    bf16x4 hi = lds_read_tr(lds + k1 * 256 + (col ^ ((k1 & 7) << 5)));
+    bf16x4 lo = lds_read_tr(lds + k0 * 256 + (col ^ (swz_mn(k0) << 5)));
+    bf16x4 hi = lds_read_tr(lds + k1 * 256 + (col ^ (swz_mn(k1) << 5)));
     return cat8(lo, hi);
   }
 }
@@ -264,7 +268,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
 constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
 constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
 
-__device__ __forceinline__ int swz_mn(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 template <bool KC>
 __device__ __forceinline__ void dma_tile(char* lds, const bf16* __restrict__ P, int64_t ld, int rows,
@@ -385,13 +388,151 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------ 256x256, staggered 4-phase ---
+// Same tile and wave grid as gemm256_kernel, re-scheduled after the MI355X guide's 8-phase
+// template (cdna_hip_programming.md §5): every K-tile is four phases, one C-quadrant (16 MFMAs)
+// each; a phase = {fragment reads for its quadrant + one half-tile LDS-DMA} | barrier |
+// {lgkmcnt(0), MFMA cluster, counted vmcnt} | barrier.  Waves 4-7 (wr = 1) run one barrier
+// behind waves 0-3, so on every SIMD one partner's MFMA cluster overlaps the other's reads.
+// The operand stream is cut into half-tiles, each holding exactly the fragments one phase reads:
+//   A_h0: rows wr*128 + {0..63}   (quadrants 0, 1)    B_h0: cols wc*64 + {0..31}  (quadrants 0, 2)
+//   A_h1: rows wr*128 + {64..127} (quadrants 2, 3)    B_h1: cols wc*64 + {32..63} (quadrants 1, 3)
+// Half-tile h (tile h/4, part order A_h0, B_h0, B_h1, A_h1) is issued in phase h-6 into a 2-deep
+// ring and retired by the counted vmcnt at the end of phase h-3; a slot is re-filled >= 2
+// phases after its last read (>= 1 for the lagging half), which the stagger's barrier order
+// makes safe (the guide's 'Read a staged buffer one phase AFTER the wait that retires it').
+constexpr int HALF = 16384;
+
+template <bool KC, bool IS_A>
+__device__ __forceinline__ void dma_half(char* lds, const bf16* __restrict__ P, int64_t ld, int rows,
+                                         int r0, int k0, int half, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wid * 2 + i;                     // 16 pieces of 1 KiB
+    const bf16* src;
+    if (KC) {          // [128 local rows][64 k], 128-B rows, chunk ^ (row & 7)
+      const int lr = piece * 8 + (lane >> 3), pc = lane & 7;
+      const int grow = IS_A ? ((lr >> 6) * 128 + ((((lr >> 4) & 3) + 4 * half) << 4) + (lr & 15))
+                            : ((lr >> 5) * 64 + ((((lr >> 4) & 1) + 2 * half) << 4) + (lr & 15));
+      const int gr = min(r0 + grow, rows - 1);
+      src = P + (int64_t)gr * ld + k0 + ((pc ^ (lr & 7)) << 3);
+    } else {           // [64 k][128 local cols], 256-B rows, 32-B granule ^ swz_mn(k)
+      const int kr = piece * 4 + (lane >> 4), pb = (lane & 15) << 4;
+      const int lc = (pb ^ (swz_mn(kr) << 5)) >> 1;
+      const int gcol = IS_A ? ((lc >> 6) * 128 + half * 64 + (lc & 63))
+                            : ((lc >> 5) * 64 + half * 32 + (lc & 31));
+      src = P + (int64_t)(k0 + kr) * ld + r0 + gcol;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A_h0|A_h1|B_h0|B_h1]
+  int tm, tn;
+  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK, nph = 4 * nk;
+  // stream part: 0 = A_h0, 1 = B_h0, 2 = B_h1, 3 = A_h1 ; slot offsets inside a 64-KiB stage
+  auto issue = [&](int T, int part) {
+    char* st = smem + (T & 1) * 2 * TILE2;
+    if (part == 0) dma_half<A_KC, true>(st, g.A, g.lda, g.M, m0, T * BK, 0, wid, lane);
+    if (part == 3) dma_half<A_KC, true>(st + HALF, g.A, g.lda, g.M, m0, T * BK, 1, wid, lane);
+    if (part == 1) dma_half<B_KC, false>(st + 2 * HALF, g.B, g.ldb, g.N, n0, T * BK, 0, wid, lane);
+    if (part == 2) dma_half<B_KC, false>(st + 3 * HALF, g.B, g.ldb, g.N, n0, T * BK, 1, wid, lane);
+  };
+  const int pro = min(6, nph);
+  for (int h = 0; h < pro; ++h) issue(h >> 2, h & 3);
+  if (pro == 6) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // phase reads: 0: A_h0 + B_h0 | 1: B_h1 | 2: A_h1 (into the A_h0 registers) | 3: none
+  bf16x8 af[4][2], bl[2][2], bh[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const char* st = smem + (t & 1) * 2 * TILE2;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int k = 4 * t + p;
+      if (p == 0 || p == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[i][s] = read_frag<A_KC>(st + (p == 0 ? 0 : HALF), wr * 64 + i * 16, s, lane);
+      }
+      if (p == 0 || p == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 f = read_frag<B_KC>(st + (p == 0 ? 2 : 3) * HALF, wc * 32 + j * 16, s, lane);
+            if (p == 0) bl[j][s] = f; else bh[j][s] = f;
+          }
+      }
+      if (k + 6 < nph) issue(t + 1 + ((p + 2) >> 2), (p + 2) & 3);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int ai = (p >> 1) * 4 + i, bj = (p & 1) * 2 + j;
+            acc[ai][bj] = mfma16((p & 1) ? bh[j][s] : bl[j][s], af[i][s], acc[ai][bj]);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      const int out = nph - 4 - k;          // half-tiles allowed in flight after this phase
+      if (out >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (out == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (out == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
+    }
+  }
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s) {
   static const bool no256 = getenv("PRFL_GEMM128") != nullptr;
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
   const bool ok256 = !no256 && (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) &&
                      (B_KC || g.N % BN2 == 0) && nt256 >= 96;
-  if (ok256) {
+  static const bool nostagger = getenv("PRFL_GEMM_NOSTAGGER") != nullptr;
+  if (ok256 && !nostagger) {
+    hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
+  } else if (ok256) {
     hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
   } else {
     const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;

@@ -40,10 +40,24 @@ if which in ("attn", "attn_bwd"):
 else:
     x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(F, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
-    for i in range(reps):
-        torch.cuda.synchronize()
-        t0 = time.time()
-        y = ops.linear(x, w)
-        torch.cuda.synchronize()
-        dt = time.time() - t0
-        print(f"gemm {L}x{F}x{C} {dt*1e3:.2f} ms  {2*L*F*C/dt/1e12:.0f} TF/s", flush=True)
+    dy = (torch.randn(L, F, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    cases = {"fwd": lambda: ops.linear(x, w), "dx": lambda: ops.linear_dx(dy, w),
+             "dw": lambda: ops.linear_dw(dy, x)}
+    # spot check against torch on a 256-row slice of the output
+    y = ops.linear(x, w).float()
+    ref = x[:256].float() @ w.float().t()
+    print("fwd rel err", ((y[:256] - ref).norm() / ref.norm()).item())
+    dx = ops.linear_dx(dy, w).float()
+    ref = dy[:256].float() @ w.float()
+    print("dx rel err", ((dx[:256] - ref).norm() / ref.norm()).item())
+    dw = ops.linear_dw(dy, x)
+    ref = dy[:, :256].float().t() @ x.float()
+    print("dw rel err", ((dw[:256] - ref).norm() / ref.norm()).item(), flush=True)
+    for name, fn in cases.items():
+        for i in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            fn()
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"gemm {name} {L}x{F}x{C} {dt*1e3:.2f} ms  {2*L*F*C/dt/1e12:.0f} TF/s", flush=True)
