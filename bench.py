@@ -108,7 +108,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="prfl_t2v_480", choices=["prfl_t2v_480", "pavrm_t2v_480"])
+    ap.add_argument("--workload", default="prfl_t2v_480",
+                    choices=["prfl_t2v_480", "prfl_t2v_720", "pavrm_t2v_480"])
     ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -117,14 +118,17 @@ def main():
     from prfl_amd import ops
     from prfl_amd.train import PAVRMTrainer, PRFLTrainer
 
-    Fl, Hl, Wl = 21, 60, 104                         # 480p x 81f latent (gen_wanx_latent.py:117-149)
+    # latents (gen_wanx_latent.py:117-149): 480p x 81f [16,21,60,104]; 720p x 81f [16,21,88,160]
+    Fl, Hl, Wl = (21, 88, 160) if args.workload.endswith("720") else (21, 60, 104)
     L = Fl * (Hl // 2) * (Wl // 2)
     gen, lrm, qa, mlp = build_models(dev, 110221)
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
-    if args.workload == "prfl_t2v_480":
-        tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0)
+    if args.workload.startswith("prfl"):
+        # 720p: AdamW moments on the host (streamed), so the whole step fits 288 GB
+        tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
+                         optimizer_state_on_host=args.workload.endswith("720"))
 
         def one(step):
             a = tr.sft_step(step, latents, text, L, generator=g)
@@ -189,8 +193,8 @@ def main():
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents/text, random-init 14B weights",
-        "config": {"workload": ("train_prfl_t2v_480: SFT + reward step, mid_timestep=%d" % args.mid
-                                if args.workload == "prfl_t2v_480" else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
+        "config": {"workload": ("train_%s: SFT + reward step, mid_timestep=%d" % (args.workload, args.mid)
+                                if args.workload.startswith("prfl") else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
                    "model": "Wan2.1-T2V-14B (40 blocks, C=5120)", "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
         "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),

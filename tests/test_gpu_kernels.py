@@ -199,6 +199,29 @@ def test_adamw_matches_torch(ops):
     assert (pd.cpu() - ref.detach()).abs().max().item() < 1e-6
 
 
+def test_adamw_host_state_streaming_is_bit_exact(ops):
+    """AdamW with moments in pinned host memory (streamed through the HBM ring) == on-device."""
+    from prfl_amd.optim import AdamW
+    g = torch.Generator().manual_seed(6)
+    shapes = [(3000,), (257, 33), (5,), (1024, 64), (7, 11)]      # more tensors than ring slots
+    base = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(3)]
+    a = [b.clone().to(DEV).requires_grad_(True) for b in base]
+    b = [x.clone().to(DEV).requires_grad_(True) for x in base]
+    oa, ob = AdamW(a), AdamW(b, state_on_host=True)
+    for gs in grads:
+        for pa, pb, gr in zip(a, b, gs):
+            pa.grad, pb.grad = gr.to(DEV), gr.to(DEV)
+        oa.step()
+        ob.step()
+    torch.cuda.synchronize()
+    for pa, pb in zip(a, b):
+        assert torch.equal(pa, pb)
+    for pa, pb in zip(a, b):
+        assert torch.equal(oa.state[pa][0].flatten().cpu(), ob.state[pb][0])
+        assert torch.equal(oa.state[pa][1].flatten().cpu(), ob.state[pb][1])
+
+
 def test_sumsq_scale(ops):
     x = torch.randn(100003, device=DEV)
     out = torch.zeros(1, device=DEV)
