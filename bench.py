@@ -1,16 +1,17 @@
 """PRFL training-step benchmark (BASELINE.json metric) on 1..8 MI355X, one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload prfl_t2v_480|pavrm_t2v_480]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload prfl_t2v_720|prfl_t2v_480|pavrm_t2v_480]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Workload (default): `configs/train_prfl_t2v_480.yaml` on one GPU per rank — the full PRFL
-iteration (flow-matching SFT step + reward step: 19-step no-grad UniPC rollout, grad-enabled
-generator step, differentiable UniPC step, 8-block latent reward model + QueryAttention + MLP,
-backward through all of it, clip, AdamW every 5th micro-step) on the 14B Wan2.1 T2V DiT
-(40 blocks, C=5120) at 480p x 81f (latent [16,21,60,104] -> L = 32760 tokens), random-init
-weights (head perturbed so gradients are non-zero), synthetic latents/text.  The 720p x 81f
-metric config does not fit a single 288 GB replica with fp32 AdamW state, so this
-is the largest single-GPU configuration in BASELINE.json `configs`.
+Workload (default): `configs/train_prfl_t2v_720.yaml` — the metric's 720p x 81f configuration
+(latent [16,21,88,160] -> L = 73920 tokens) — one sample per GPU: the full PRFL iteration
+(flow-matching SFT step + reward step: 19-step no-grad UniPC rollout, grad-enabled generator
+step, differentiable UniPC step, 8-block latent reward model + QueryAttention + MLP, backward
+through all of it, clip, AdamW every 5th micro-step; the timed window ends on an optimizer step)
+on the 14B Wan2.1 T2V DiT (40 blocks, C=5120), random-init weights (head perturbed so gradients
+are non-zero), synthetic latents/text.  Memory plan: on one GPU the AdamW moments
+live in pinned host memory and stream through HBM during the step; with N ranks they are
+ZeRO-1 sharded across the GPUs.  `--workload prfl_t2v_480` runs the 480p x 81f config (L=32760).
 
 Multi-GPU: pure data parallel (weak scaling, one sample per rank), RCCL all-reduce of the
 generator gradients overlapped with the backward (prfl_amd/dist.py).  `value` = PRFL sample-
@@ -103,18 +104,32 @@ def cpu_baseline(L_sample=4096):
     return dt, flops, threads
 
 
+def heartbeat(period=60.0):
+    """A progress line on stderr every `period` s (a 720p iteration runs for minutes)."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print(f"[bench] alive {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="prfl_t2v_480",
+    ap.add_argument("--workload", default="prfl_t2v_720",
                     choices=["prfl_t2v_480", "prfl_t2v_720", "pavrm_t2v_480"])
     ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     world, rank, local = setup()
     dev = torch.device("cuda", local)
+    if rank == 0:
+        heartbeat()
     from prfl_amd import ops
     from prfl_amd.train import PAVRMTrainer, PRFLTrainer
 
@@ -126,9 +141,11 @@ def main():
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
     if args.workload.startswith("prfl"):
-        # 720p: AdamW moments on the host (streamed), so the whole step fits 288 GB
+        # 720p memory plan: one GPU keeps the AdamW moments on the host (streamed);
+        # with DP ranks they are ZeRO-1 sharded on the devices instead
+        big = args.workload.endswith("720")
         tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
-                         optimizer_state_on_host=args.workload.endswith("720"))
+                         optimizer_state_on_host=big and world == 1, optimizer_shard=big and world > 1)
 
         def one(step):
             a = tr.sft_step(step, latents, text, L, generator=g)

@@ -1,15 +1,17 @@
 """Data-parallel gradient exchange for the PRFL step (replaces FSDP FULL_SHARD + Ulysses SP of
 `fsdp_utils.py:66-122` / `communication.py:40-160` with pure batch DP over RCCL/xGMI).
 
-Every rank holds a full replica (288 GB HBM fits the 14B fp32 master + AdamW state at 480p).
+Every rank holds a full replica of the weights.
 The reference reduces the FRESH gradient of every backward (FSDP reduce-scatters each micro-step,
-no `no_sync`) and accumulates the reduced gradient; `GradReducer` does the same:
+no `no_sync`) and accumulates the reduced gradient.  Because the accumulated part is already
+identical on every rank, avg_r(acc + fresh_r) = acc + avg_r(fresh_r): `GradReducer` lets autograd
+accumulate in place into .grad and all-reduces the sum, which needs no second gradient buffer
+(57 GB for the 14B DiT in fp32 - what makes the 720p step fit):
 
-  before backward : stash accumulated grads, clear .grad
   during backward : a post-accumulate-grad hook fires per parameter as soon as its block's fused
                     backward node returns (reverse layer order) and launches an async all-reduce
                     on RCCL's stream -> communication overlaps the remaining blocks' backward
-  after backward  : wait, average (gloo has no AVG), add the stash back
+  after backward  : wait; average (gloo has no AVG)
 
 Block gradients are 105-283 MB tensors, well past the point where a ring all-reduce is
 bandwidth-bound on xGMI, so tensors are reduced individually (no flatten/copy buckets); the
@@ -29,7 +31,6 @@ class GradReducer:
         self.world = dist.get_world_size() if is_dist() else 1
         self.small_numel = small_numel
         self.works = []
-        self.stash = {}
         self.small_pending = []
         self.backend = dist.get_backend() if is_dist() else None
         self.handles = []
@@ -57,14 +58,11 @@ class GradReducer:
         self.works.append((w, (flat, ps)))
 
     def begin(self):
-        """Call before loss.backward()."""
-        for p in self.params:
-            if p.grad is not None:
-                self.stash[p] = p.grad
-                p.grad = None
+        """Call before loss.backward() (kept for the driver's call pattern; nothing to stash)."""
+        self.works = []
 
     def end(self):
-        """Call after loss.backward(): completes the exchange and re-accumulates."""
+        """Call after loss.backward(): completes the exchange."""
         if self.world > 1:
             self._flush_small()
             for w, payload in self.works:
@@ -81,13 +79,6 @@ class GradReducer:
                 elif self.backend != "nccl":
                     payload[0].div_(self.world)
             self.works = []
-        for p, g in self.stash.items():
-            if p.grad is None:
-                p.grad = g
-            else:
-                g.add_(p.grad)
-                p.grad = g
-        self.stash = {}
 
 
 def broadcast_int(v, src=0, device="cpu"):

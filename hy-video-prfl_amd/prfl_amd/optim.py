@@ -7,6 +7,10 @@
                         memory and streams them through a 3-slot HBM ring on two copy streams
                         (H2D of tensor i+1 and D2H of tensor i-1 overlap the kernel on tensor i):
                         the memory plan that fits 720p x 81f on one 288 GB GPU.
+                        ``shard=True`` (data parallel, world > 1): ZeRO-1 — every rank keeps the
+                        moments of, and updates, only the tensors it owns (size-balanced, the same
+                        assignment on every rank), then each tensor is broadcast from its owner;
+                        parameters stay bit-identical to the replicated update.
 * ``clip_grad_norm_`` — global L2 norm over all grads and in-place scaling by
                         min(1, max_norm/(norm+1e-6)) (`train_prfl.py:825,972`), with the clip
                         coefficient kept on the device (no host synchronisation).
@@ -18,8 +22,19 @@ from . import ops
 
 class AdamW:
     def __init__(self, params, lr=5e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                 state_on_host=False, ring_slots=3):
+                 state_on_host=False, ring_slots=3, shard=False):
         self.params = [p for p in params if p.requires_grad]
+        self.shard = shard
+        if shard:
+            import torch.distributed as dist
+            self.rank, self.world = dist.get_rank(), dist.get_world_size()
+            loads = [0] * self.world
+            self.owner = {}
+            order = sorted(range(len(self.params)), key=lambda i: (-self.params[i].numel(), i))
+            for i in order:
+                r = min(range(self.world), key=lambda k: (loads[k], k))
+                self.owner[self.params[i]] = r
+                loads[r] += self.params[i].numel()
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.state = {}
         self.step_count = 0
@@ -45,6 +60,15 @@ class AdamW:
         self.step_count += 1
         lr = self.param_groups[0]["lr"]
         live = [p for p in self.params if p.grad is not None]
+        if self.shard:
+            import torch.distributed as dist
+            self._update([p for p in live if self.owner[p] == self.rank], lr)
+            for p in live:
+                dist.broadcast(p.data, src=self.owner[p])
+            return
+        self._update(live, lr)
+
+    def _update(self, live, lr):
         if self.state_on_host:
             return self._step_streamed(live, lr)
         for p in live:
@@ -100,6 +124,13 @@ class AdamW:
 
     def state_bytes(self):
         return sum(2 * p.numel() * 4 for p in self.state)
+
+    def state_dict(self):
+        """Moments of the tensors this rank holds (host or device), by parameter index."""
+        idx = {id(p): i for i, p in enumerate(self.params)}
+        return {"step": self.step_count,
+                "state": {idx[id(p)]: {"exp_avg": m.view_as(p), "exp_avg_sq": v.view_as(p)}
+                          for p, (m, v) in self.state.items()}}
 
 
 @torch.no_grad()

@@ -54,3 +54,57 @@ def test_grad_reducer_gloo_world2():
     for n, p in model.named_parameters():
         assert torch.allclose(g0[n], p.grad, atol=1e-6, rtol=1e-5), n
         assert torch.equal(g0[n], g1[n]), n
+
+
+def _adamw_ref(p, g, m, v, lr, b1, b2, eps, wd, step):
+    """torch.optim.AdamW update (the prfl_adamw kernel's contract) for the CPU test."""
+    p.mul_(1 - lr * wd)
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    denom = (v / (1 - b2 ** step)).sqrt_().add_(eps)
+    p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
+
+
+def _zero1_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from prfl_amd import optim
+    optim.ops.adamw_ = _adamw_ref
+    torch.manual_seed(0)
+    ps = [torch.randn(s).requires_grad_(True) for s in [(64, 33), (1000,), (7,), (300, 3), (5, 5)]]
+    opt = optim.AdamW(ps, lr=1e-2, shard=True)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(3):
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g)    # identical on both ranks (post all-reduce)
+        opt.step()
+    owned = sorted(i for i, p in enumerate(ps) if opt.owner[p] == rank)
+    out_q.put((rank, [p.detach().clone() for p in ps], owned, len(opt.state)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero1_adamw_gloo_world2():
+    """ZeRO-1 AdamW: each rank holds half the moments; parameters equal the replicated update."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_zero1_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, p0, own0, n0), (_, p1, own1, n1) = res
+    assert sorted(own0 + own1) == list(range(5)) and not set(own0) & set(own1)
+    assert n0 == len(own0) and n1 == len(own1)
+    torch.manual_seed(0)
+    ref = [torch.randn(s) for s in [(64, 33), (1000,), (7,), (300, 3), (5, 5)]]
+    st = [(torch.zeros_like(p), torch.zeros_like(p)) for p in ref]
+    g = torch.Generator().manual_seed(1)
+    for step in range(1, 4):
+        for p, (m, v) in zip(ref, st):
+            _adamw_ref(p, torch.randn(p.shape, generator=g), m, v, 1e-2, 0.9, 0.999, 1e-8, 0.01, step)
+    for a, b, r in zip(p0, p1, ref):
+        assert torch.equal(a, b) and torch.equal(a, r)
