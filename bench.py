@@ -25,6 +25,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# fewer, growable segments: the 720p step's live set is ~220 GB of mixed-size tensors
+os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hy-video-prfl_amd")]
 
 import torch  # noqa: E402
@@ -141,11 +143,12 @@ def main():
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
     if args.workload.startswith("prfl"):
-        # 720p memory plan: one GPU keeps the AdamW moments on the host (streamed);
-        # with DP ranks they are ZeRO-1 sharded on the devices instead
+        # 720p memory plan: the AdamW moments live in pinned host memory and stream
+        # through HBM during the step; with DP ranks they are also ZeRO-1 sharded (each rank
+        # holds and streams 1/N of them, then broadcasts the tensors it updated)
         big = args.workload.endswith("720")
         tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
-                         optimizer_state_on_host=big and world == 1, optimizer_shard=big and world > 1)
+                         optimizer_state_on_host=big, optimizer_shard=big and world > 1)
 
         def one(step):
             a = tr.sft_step(step, latents, text, L, generator=g)
