@@ -42,6 +42,24 @@ __device__ __forceinline__ bf16x4 lds_read_tr(const void* lds_byte_addr) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// LDS-DMA of one 16-B chunk per lane (global_load_lds_dwordx4) issued from inline asm, so the
+// compiler's waitcnt bookkeeping does not see an LDS write it cannot disambiguate (hipcc would
+// otherwise put vmcnt(0) before every ds_read_b64_tr_b16 and drain the prefetch).  The caller
+// owns completion: counted `s_waitcnt vmcnt(N)` + barrier before any ds_read of the bytes.
+// lds_dst is the wave-uniform LDS byte address of the 1-KiB piece (lane i lands at +16 i).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+      : "memory");
+}
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }

@@ -285,9 +285,7 @@ __device__ __forceinline__ void dma_tile(char* lds, const bf16* __restrict__ P, 
       const int lb = pb ^ (swz_mn(kr) << 5);
       src = P + (int64_t)(k0 + kr) * ld + r0 + (lb >> 1);
     }
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024),
-                                     16, 0, 0);
+    dma16(src, lds_addr(lds + piece * 1024));
   }
 }
 
@@ -423,9 +421,7 @@ __device__ __forceinline__ void dma_half(char* lds, const bf16* __restrict__ P, 
                             : ((lc >> 5) * 64 + half * 32 + (lc & 31));
       src = P + (int64_t)(k0 + kr) * ld + r0 + gcol;
     }
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024),
-                                     16, 0, 0);
+    dma16(src, lds_addr(lds + piece * 1024));
   }
 }
 

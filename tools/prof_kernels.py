@@ -11,7 +11,7 @@ from prfl_amd import ops  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "attn"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-L, C, NH, F = 32760, 5120, 40, 13824
+L, C, NH, F = int(os.environ.get("PRFL_PROF_L", 32760)), 5120, 40, 13824
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
 if which in ("attn", "attn_bwd"):
