@@ -10,7 +10,9 @@ rocprofv3 -L > $out/counters.txt 2>&1 || true
 passes=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES"
         "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
         "FETCH_SIZE"
-        "WRITE_SIZE")
+        "WRITE_SIZE"
+        "SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE")
+[ -n "$PMC_PASSES" ] && passes=("${passes[@]:$PMC_PASSES}")
 for w in $which; do
   i=0
   for p in "${passes[@]}"; do
