@@ -148,7 +148,9 @@ def main():
         # holds and streams 1/N of them, then broadcasts the tensors it updated)
         big = args.workload.endswith("720")
         tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
-                         optimizer_state_on_host=big, optimizer_shard=big and world > 1)
+                         optimizer_state_on_host=big or os.environ.get("PRFL_OPT_HOST") == "1",
+                         optimizer_shard=big and world > 1,
+                         optimizer_overlap=os.environ.get("PRFL_OPT_OVERLAP", "1") == "1")
 
         def one(step):
             a = tr.sft_step(step, latents, text, L, generator=g)

@@ -1015,6 +1015,151 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv32_kernel(AttnBwdArgs a) 
   }
 }
 
+// dK, dV with 8 waves (two per SIMD): 256 keys per workgroup, 32 per wave with the K^T
+// fragments and the dK^T / dV^T accumulators resident; V of the workgroup's keys is staged once
+// in LDS (the B operand of dP = dO.V^T is re-read per query slice) so a wave fits the 256
+// registers that two waves per SIMD allow.  Q / dO tiles of 64 queries and their LSE / D rows
+// arrive by LDS-DMA into a 2-stage ring, one barrier per tile: tile t+1 is issued at the top of
+// tile t into the stage tile t-1 used (all waves are past the barrier that ended tile t-1) and
+// retired by vmcnt(0) + the barrier that ends tile t.  Per-element arithmetic and its order are
+// those of attn_bwd_dkdv32_kernel (bit-identical results).
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_kernel(AttnBwdArgs a) {
+  constexpr int V_BYTES = 256 * 256, STAGE = 16384 * 2 + 512;
+  __shared__ __attribute__((aligned(16))) char smem[V_BYTES + 2 * STAGE];
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
+  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
+  const int key = k0 + w * 32 + l32;
+  const bool kvalid = key < a.k_len;
+  const int kr = min(key, a.Lk - 1);
+  bf16x8 kf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kf[ks] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ks * 16 + hh * 8);
+  char* Vs = smem;
+  // V rows of the 256 keys (off16 image, row reads): 64 pieces of 4 rows, 8 per wave
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = w * 8 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+    const int kk = min(k0 + row, a.Lk - 1);
+    dma16(Vb + (int64_t)kk * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
+  }
+  // Q / dO tile (offB image, row and transposed reads): 16 + 16 pieces, 4 per wave; LSE, D rows
+  auto dma_tile = [&](int t, int st) {
+    char* Qs = smem + V_BYTES + st * STAGE;
+    char* Ds = Qs + 16384;
+    const int qb = t * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = w * 2 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+      const int q = min(qb + row, a.Lq - 1);
+      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+      dma16(Qb + (int64_t)q * a.ldq + ((pc ^ swzb) << 3), lds_addr(Qs + piece * 1024));
+      dma16(dOb + (int64_t)q * a.lddo + ((pc ^ swzb) << 3), lds_addr(Ds + piece * 1024));
+    }
+    if (w < 2) {
+      const int q = min(qb + lane, a.Lq - 1);
+      dma4((w == 0 ? lseb : delb) + q, lds_addr(Qs + 32768 + w * 256));
+    }
+  };
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  const int nq = (a.Lq + 63) / 64;
+  dma_tile(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): K fragments, V, tile 0
+  __syncthreads();
+  for (int t = 0; t < nq; ++t) {
+    const int st = t & 1;
+    if (t + 1 < nq) dma_tile(t + 1, st ^ 1);
+    const char* Qs = smem + V_BYTES + st * STAGE;
+    const char* Ds = Qs + 16384;
+    const float* Ls = (const float*)(Qs + 32768);
+    const int qb = t * 64;
+    const bool tail = qb + 64 > a.Lq;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 sacc, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpt[r] = 0.f; }
+      const int row = qt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        sacc = mfma32(*(const bf16x8*)(Qs + offB(row, (ks * 2 + hh) * 16)), kf[ks], sacc);
+        const bf16x8 vfr = *(const bf16x8*)(Vs + off16(w * 32 + l32, ks * 2 + hh));
+        dpt = mfma32(*(const bf16x8*)(Ds + offB(row, (ks * 2 + hh) * 16)), vfr, dpt);
+        if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      // rows q = qb + qt*32 + (r&3) + 8(r>>2) + 4hh
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int q4 = qt * 32 + 8 * rg + 4 * hh;
+        const f32x4 l4 = *(const f32x4*)(Ls + q4);
+        const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = kvalid ? __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]) : 0.f;
+          if (tail && qb + q4 + r >= a.Lq) p = 0.f;
+          sacc[rg * 4 + r] = p;
+          dpt[rg * 4 + r] = p * (dpt[rg * 4 + r] - d4[r]);
+        }
+      }
+      bf16x8 pk[2], dk8[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pk[s2] = (bf16x8){f2bf(sacc[8 * s2 + 0]), f2bf(sacc[8 * s2 + 1]), f2bf(sacc[8 * s2 + 2]),
+                          f2bf(sacc[8 * s2 + 3]), f2bf(sacc[8 * s2 + 4]), f2bf(sacc[8 * s2 + 5]),
+                          f2bf(sacc[8 * s2 + 6]), f2bf(sacc[8 * s2 + 7])};
+        dk8[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                           f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                           f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = qt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const bf16x8 dof = cat8(lds_read_tr(Ds + offB(ra, byte)), lds_read_tr(Ds + offB(ra + 8, byte)));
+          const bf16x8 qtf = cat8(lds_read_tr(Qs + offB(ra, byte)), lds_read_tr(Qs + offB(ra + 8, byte)));
+          dv[dt] = mfma32(dof, pk[s2], dv[dt]);
+          dk[dt] = mfma32(qtf, dk8[s2], dk[dt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (key < a.Lk) {
+    bf16* dKb = a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk;
+    bf16* dVb = a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 vk, vv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vk[r] = f2bf(dk[dt][rg * 4 + r] * a.scale);
+          vv[r] = f2bf(dv[dt][rg * 4 + r]);
+        }
+        *(bf16x4*)(dKb + dt * 32 + 8 * rg + 4 * hh) = vk;
+        *(bf16x4*)(dVb + dt * 32 + 8 * rg + 4 * hh) = vv;
+      }
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
@@ -1076,11 +1221,14 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
                 scale * 1.4426950408889634f, scale};
   static const bool bwd16 = getenv("PRFL_ATTN_BWD16") != nullptr;
+  static const bool dkdv4 = getenv("PRFL_ATTN_DKDV4") != nullptr;
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
   if (bwd16)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
-  else
+  else if (dkdv4)
     hipLaunchKernelGGL(attn_bwd_dkdv32_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv8_kernel, dim3((Lk + 255) / 256, H, B), dim3(512), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();

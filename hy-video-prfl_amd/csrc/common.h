@@ -60,6 +60,17 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
       : "memory");
 }
 
+// 4-B-per-lane variant (global_load_lds_dword): lane i lands at lds_dst + 4 i.
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+      : "memory");
+}
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }

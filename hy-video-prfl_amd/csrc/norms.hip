@@ -27,29 +27,34 @@ __device__ __forceinline__ f32x4 ld4(const void* p, int64_t i, int is_bf16) {
 __device__ __forceinline__ f32x4 ldf4(const float* p, int i) { return *(const f32x4*)(p + i); }
 
 // --------------------------------------------------------------------------- LN + modulate --
+// One wave per row (4 rows per 256-thread workgroup): the row (C <= 5120 -> 20 float4 chunks per
+// lane) stays in registers, both reductions are wave shuffles (no LDS, no barriers), so a CU keeps
+// many rows in flight and the kernel streams at HBM rate.  Two-pass mean / variance as before.
+constexpr int WV = 20;  // float4 chunks per lane -> C <= 5120
 __global__ __launch_bounds__(NT) void ln_mod_fwd_kernel(
-    const void* __restrict__ x, int x_bf16, int64_t ldx, int C, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ w, const float* __restrict__ b,
-    float eps, bf16* __restrict__ out, int64_t ldo, float* __restrict__ mean_out,
-    float* __restrict__ rstd_out) {
-  __shared__ float red[NT / 64];
-  const int64_t row = blockIdx.x;
+    const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ w,
+    const float* __restrict__ b, float eps, bf16* __restrict__ out, int64_t ldo,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= L) return;
+  const int lane = threadIdx.x & 63;
   const int nc = C / 4;
-  f32x4 v[MAXV];
+  f32x4 v[WV];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = threadIdx.x + j * NT;
+  for (int j = 0; j < WV; ++j) {
+    const int c = lane + j * 64;
     if (c < nc) {
       v[j] = ld4(x, row * ldx + c * 4, x_bf16);
       s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
     }
   }
-  const float mean = block_sum<NT>(s, red) / C;
+  const float mean = wave_sum(s) / C;
   float ss = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = threadIdx.x + j * NT;
+  for (int j = 0; j < WV; ++j) {
+    const int c = lane + j * 64;
     if (c < nc) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -58,11 +63,11 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_kernel(
       }
     }
   }
-  const float var = block_sum<NT>(ss, red) / C;
+  const float var = wave_sum(ss) / C;
   const float rstd = rsqrtf(var + eps);
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = threadIdx.x + j * NT;
+  for (int j = 0; j < WV; ++j) {
+    const int c = lane + j * 64;
     if (c < nc) {
       bf16x4 o;
       f32x4 a = w ? ldf4(w, c * 4) : (f32x4){0, 0, 0, 0};
@@ -84,7 +89,7 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_kernel(
       *(bf16x4*)(out + row * ldo + c * 4) = o;
     }
   }
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
   }
@@ -318,8 +323,9 @@ extern "C" int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L
   if (bad_c(C) || (!w && (!scale || !shift))) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  hipLaunchKernelGGL(ln_mod_fwd_kernel, dim3(L), dim3(NT), 0, s, x, x_bf16, ldx, (int)C, scale,
-                     shift, w, b, eps, (bf16*)out, ldo, mean, rstd);
+  hipLaunchKernelGGL(ln_mod_fwd_kernel, dim3((L + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, s, x,
+                     x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps, (bf16*)out, ldo, mean,
+                     rstd);
   prfl_prof::set_work((double)L * C * ((x_bf16 ? 2 : 4) + 2));
   prfl_prof::end(KID_LN, s);
   PRFL_LAUNCH_CHECK();

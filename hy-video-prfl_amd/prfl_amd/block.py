@@ -265,7 +265,7 @@ class WanBlockFn(torch.autograd.Function):
         del W
         fctx.meta, fctx.names = meta, names
         fctx.save_for_backward(x, e, context, *params)
-        return torch.stack(outs)
+        return outs[0].unsqueeze(0) if len(outs) == 1 else torch.stack(outs)
 
     @staticmethod
     def backward(fctx, dout):
@@ -284,7 +284,7 @@ class WanBlockFn(torch.autograd.Function):
             dxs.append(dx)
             des.append(de)
             dcs.append(dc)
-        dx = torch.stack(dxs).to(x.dtype)
+        dx = (dxs[0].unsqueeze(0) if len(dxs) == 1 else torch.stack(dxs)).to(x.dtype)
         de = torch.stack(des)
         dctx = torch.stack(dcs).to(context.dtype) if context.requires_grad else None
         pg = [G.get(n) if p.requires_grad else None for n, p in zip(names, params)]

@@ -2,15 +2,24 @@
 
 * ``AdamW``           — torch.optim.AdamW semantics (`train_prfl.py:479-491`: lr 5e-6, betas
                         (0.9, 0.999), eps 1e-8, weight decay 0.01), fp32 state, one HBM-bound
-                        kernel per parameter tensor (prfl_adamw).  ``state_on_host=True`` keeps
-                        exp_avg / exp_avg_sq (8 B/param, 114 GB for the 14B DiT) in pinned host
-                        memory and streams them through a 3-slot HBM ring on two copy streams
-                        (H2D of tensor i+1 and D2H of tensor i-1 overlap the kernel on tensor i):
-                        the memory plan that fits 720p x 81f on one 288 GB GPU.
-                        ``shard=True`` (data parallel, world > 1): ZeRO-1 — every rank keeps the
-                        moments of, and updates, only the tensors it owns (size-balanced, the same
-                        assignment on every rank), then each tensor is broadcast from its owner;
-                        parameters stay bit-identical to the replicated update.
+                        kernel per parameter tensor (prfl_adamw).
+    ``state_on_host`` keeps exp_avg / exp_avg_sq (8 B/param, 114 GB for the 14B DiT) in pinned
+                      host memory and streams them through a small HBM ring: the memory plan that
+                      fits 720p x 81f on one 288 GB GPU.  Both directions share ONE
+                      copy stream: the host link moves 57 GB/s one way at a time but only
+                      ~37 GB/s in total when H2D and D2H run concurrently (profiles/r01_pcie.txt).
+    ``overlap``       the update runs on a side stream and step() returns without making the
+                      caller's stream wait.  Every parameter gets a ready event; ``attach(model)``
+                      installs forward pre-hooks so the first forward that reads a parameter
+                      (block by block) waits for exactly that parameter's update.  The streamed
+                      update of block i thus runs under the forwards of blocks < i (the SFT
+                      step's update hides under the reward step's no-grad rollout).  Results are
+                      bit-identical to the synchronous update: same kernel, same inputs, and every
+                      reader is ordered after the write.
+    ``shard``         (data parallel, world > 1): ZeRO-1 — every rank keeps the moments of, and
+                      updates, only the tensors it owns (size-balanced, the same assignment on
+                      every rank), then each tensor is broadcast from its owner; parameters stay
+                      bit-identical to the replicated update.
 * ``clip_grad_norm_`` — global L2 norm over all grads and in-place scaling by
                         min(1, max_norm/(norm+1e-6)) (`train_prfl.py:825,972`), with the clip
                         coefficient kept on the device (no host synchronisation).
@@ -22,7 +31,7 @@ from . import ops
 
 class AdamW:
     def __init__(self, params, lr=5e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                 state_on_host=False, ring_slots=3, shard=False):
+                 state_on_host=False, ring_slots=3, shard=False, overlap=False):
         self.params = [p for p in params if p.requires_grad]
         self.shard = shard
         if shard:
@@ -39,8 +48,12 @@ class AdamW:
         self.state = {}
         self.step_count = 0
         self.state_on_host = state_on_host
+        self.overlap = overlap
         self.ring_slots = ring_slots
         self._ring = None
+        self._streams = None
+        self._ready = {}            # param -> event (optimizer stream) after its final write
+        self._hooks = []
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                   params=self.params)]
 
@@ -55,68 +68,160 @@ class AdamW:
             self.state[p] = st
         return st
 
+    def init_state(self):
+        """Allocate the moments now (zeros, as torch.optim.AdamW's lazy first step does) instead
+        of inside the first step: pinning 114 GB of host memory takes ~10 s, a one-time cost."""
+        for p in self.params:
+            if not self.shard or self.owner[p] == self.rank:
+                self._state(p)
+
+    # ------------------------------------------------------------------ ordering ----------
+    def wait(self, params=None):
+        """Make the current stream wait for the pending updates of `params` (default: all)."""
+        if not self._ready:
+            return
+        ps = list(self._ready) if params is None else [p for p in params if p in self._ready]
+        if not ps:
+            return
+        cur = torch.cuda.current_stream(ps[0].device)
+        for p in ps:
+            cur.wait_event(self._ready.pop(p))
+
+    def synchronize(self):
+        """All updates visible to the current stream and the host moments complete."""
+        self.wait()
+        if self._streams is not None:
+            for s in self._streams:
+                s.synchronize()
+
+    def attach(self, model, groups=None):
+        """Forward pre-hooks: each module in `groups` (default: every element of model.blocks,
+        then model.head) waits for its own parameters' updates; `model` itself waits for the
+        remaining ones (embeddings), which are therefore updated first: the update order becomes
+        [rest, groups...] = the order in which a forward first reads them."""
+        if groups is None:
+            groups = list(model.blocks) + ([model.head] if getattr(model, "head", None) is not None
+                                           else [])
+        inner = {id(p) for g in groups for p in g.parameters()}
+        rest = [p for p in model.parameters() if id(p) not in inner]
+        order = {id(p): i for i, p in enumerate(rest + [p for g in groups for p in g.parameters()])}
+        self.params.sort(key=lambda p: order.get(id(p), len(order)))
+        self._hooks.append(model.register_forward_pre_hook(lambda m, a: self.wait(rest)))
+        for g in groups:
+            ps = list(g.parameters())
+            self._hooks.append(g.register_forward_pre_hook(lambda m, a, ps=ps: self.wait(ps)))
+
+    # ------------------------------------------------------------------ update ------------
     @torch.no_grad()
     def step(self):
         self.step_count += 1
         lr = self.param_groups[0]["lr"]
         live = [p for p in self.params if p.grad is not None]
-        if self.shard:
-            import torch.distributed as dist
-            self._update([p for p in live if self.owner[p] == self.rank], lr)
-            for p in live:
-                dist.broadcast(p.data, src=self.owner[p])
+        if not live:
             return
-        self._update(live, lr)
+        if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
+            return self._step_cpu(live, lr)
+        dev = live[0].device
+        main = torch.cuda.current_stream(dev)
+        if self._streams is None:
+            self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+        opt, cp = self._streams
+        self.wait(live)                             # a previous step still in flight
+        opt.wait_stream(main)                       # grads (clipped) and params are final
+        mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
+        with torch.cuda.stream(opt):
+            if self.state_on_host:
+                done = self._update_streamed(mine, lr, opt, cp)
+            else:
+                done = self._update_device(mine, lr)
+            if self.shard:
+                import torch.distributed as dist
+                for p in live:
+                    if p in done:
+                        opt.wait_event(done[p])
+                    dist.broadcast(p.data, src=self.owner[p], async_op=True).wait()
+                    ev = torch.cuda.Event()
+                    ev.record(opt)
+                    self._ready[p] = ev
+            else:
+                self._ready.update(done)
+        for p in live:                              # grads are read on the side stream
+            p.grad.record_stream(opt)
+        if not self.overlap:
+            self.wait(live)
 
-    def _update(self, live, lr):
-        if self.state_on_host:
-            return self._step_streamed(live, lr)
+    def _update_device(self, live, lr):
+        done = {}
         for p in live:
             m, v = self._state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             ops.adamw_(p.data, g, m, v, lr, self.betas[0], self.betas[1], self.eps,
                        self.weight_decay, self.step_count)
+            ev = torch.cuda.Event()
+            ev.record()
+            done[p] = ev
+        return done
 
-    def _step_streamed(self, live, lr):
+    def _update_streamed(self, live, lr, opt, cp):
+        """Moments host -> ring -> kernel -> host, one copy stream for both directions: copy
+        stream order H2D(0..k-1), then per tensor i: D2H(i) after kernel(i), H2D(i+k) into the
+        slot D2H(i) just drained."""
+        done = {}
         if not live:
-            return
+            return done
         dev = live[0].device
         nmax = max(p.numel() for p in live)
-        if self._ring is None or self._ring[0].numel() < 2 * nmax:
-            k = self.ring_slots
-            self._ring = [torch.empty(2 * nmax, dtype=torch.float32, device=dev) for _ in range(k)]
-            self._h2d = torch.cuda.Stream(device=dev)
-            self._d2h = torch.cuda.Stream(device=dev)
-            self._ev = [[torch.cuda.Event() for _ in range(3)] for _ in range(k)]  # h2d, kernel, d2h
-            self._used = [False] * k
-        main = torch.cuda.current_stream(dev)
         k = self.ring_slots
-        for i, p in enumerate(live):
-            j = i % k
-            n = p.numel()
+        if self._ring is None or self._ring[0].numel() < 2 * nmax:
+            self._ring = [torch.empty(2 * nmax, dtype=torch.float32, device=dev) for _ in range(k)]
+            for b in self._ring:
+                b.record_stream(cp)
+        slots = [(b[:nmax], b[nmax:2 * nmax]) for b in self._ring]
+        h2d_ev = [None] * len(live)
+
+        def h2d(i):
+            p = live[i]
             m_h, v_h = self._state(p)
-            buf = self._ring[j]
-            m_d, v_d = buf[:n], buf[nmax:nmax + n]
-            ev_h2d, ev_k, ev_d2h = self._ev[j]
-            with torch.cuda.stream(self._h2d):
-                if self._used[j]:
-                    self._h2d.wait_event(ev_d2h)          # slot's previous tensor written back
-                m_d.copy_(m_h, non_blocking=True)
-                v_d.copy_(v_h, non_blocking=True)
-                ev_h2d.record(self._h2d)
-            main.wait_event(ev_h2d)
+            m_d, v_d = slots[i % k]
+            n = p.numel()
+            with torch.cuda.stream(cp):
+                m_d[:n].copy_(m_h, non_blocking=True)
+                v_d[:n].copy_(v_h, non_blocking=True)
+                h2d_ev[i] = torch.cuda.Event()
+                h2d_ev[i].record(cp)
+
+        # the ring is reused across steps: the previous step's D2H are earlier on `cp`
+        for i in range(min(k, len(live))):
+            h2d(i)
+        for i, p in enumerate(live):
+            n = p.numel()
+            m_d, v_d = slots[i % k]
+            opt.wait_event(h2d_ev[i])
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            ops.adamw_(p.data, g, m_d.view_as(p), v_d.view_as(p), lr, self.betas[0], self.betas[1],
-                       self.eps, self.weight_decay, self.step_count)
-            ev_k.record(main)
-            with torch.cuda.stream(self._d2h):
-                self._d2h.wait_event(ev_k)
-                m_h.copy_(m_d, non_blocking=True)
-                v_h.copy_(v_d, non_blocking=True)
-                ev_d2h.record(self._d2h)
-            self._used[j] = True
-        # the host state must be complete before anyone reads it; the ring before it is reused
-        main.wait_stream(self._d2h)
+            ops.adamw_(p.data, g, m_d[:n].view_as(p), v_d[:n].view_as(p), lr, self.betas[0],
+                       self.betas[1], self.eps, self.weight_decay, self.step_count)
+            ev = torch.cuda.Event()
+            ev.record(opt)
+            done[p] = ev
+            m_h, v_h = self._state(p)
+            with torch.cuda.stream(cp):
+                cp.wait_event(ev)
+                m_h.copy_(m_d[:n], non_blocking=True)
+                v_h.copy_(v_d[:n], non_blocking=True)
+            if i + k < len(live):
+                h2d(i + k)
+        return done
+
+    def _step_cpu(self, live, lr):
+        mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
+        for p in mine:
+            m, v = self._state(p)
+            ops.adamw_(p.data, p.grad, m, v, lr, self.betas[0], self.betas[1], self.eps,
+                       self.weight_decay, self.step_count)
+        if self.shard:
+            import torch.distributed as dist
+            for p in live:
+                dist.broadcast(p.data, src=self.owner[p])
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:
@@ -127,6 +232,7 @@ class AdamW:
 
     def state_dict(self):
         """Moments of the tensors this rank holds (host or device), by parameter index."""
+        self.synchronize()
         idx = {id(p): i for i, p in enumerate(self.params)}
         return {"step": self.step_count,
                 "state": {idx[id(p)]: {"exp_avg": m.view_as(p), "exp_avg_sq": v.view_as(p)}

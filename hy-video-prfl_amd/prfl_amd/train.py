@@ -46,12 +46,19 @@ def build_lrm(model, trainable_blocks=range(8)):
 class PRFLTrainer:
     def __init__(self, transformer, lrm, query_attention, mlp, lr=5e-6, weight_decay=0.01,
                  grad_accum=5.0, flow_shift=5.0, inference_steps=40, feature_layer=(8,),
-                 max_grad_norm=1.0, optimizer_state_on_host=False, optimizer_shard=False):
+                 max_grad_norm=1.0, optimizer_state_on_host=False, optimizer_shard=False,
+                 optimizer_overlap=True):
         self.transformer, self.lrm, self.qa, self.mlp = transformer, lrm, query_attention, mlp
         params = [p for p in transformer.parameters() if p.requires_grad]
         self.params = params
         self.optimizer = AdamW(params, lr=lr, weight_decay=weight_decay,
-                               state_on_host=optimizer_state_on_host, shard=optimizer_shard)
+                               state_on_host=optimizer_state_on_host, shard=optimizer_shard,
+                               overlap=optimizer_overlap)
+        self.optimizer.init_state()
+        if optimizer_overlap:
+            # each block's forward waits for its own parameters' update (optim.py): the SFT
+            # step's optimizer update streams under the reward step's rollout
+            self.optimizer.attach(transformer)
         self.reducer = GradReducer(params)
         self.grad_accum = grad_accum
         self.inference_steps = inference_steps

@@ -222,6 +222,50 @@ def test_adamw_host_state_streaming_is_bit_exact(ops):
         assert torch.equal(oa.state[pa][1].flatten().cpu(), ob.state[pb][1])
 
 
+def test_adamw_overlapped_update_is_bit_exact(ops):
+    """overlap=True (update on a side stream, readers ordered by per-parameter events installed
+    as forward pre-hooks) == the synchronous update, with host-streamed and device moments."""
+    from prfl_amd.optim import AdamW
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Linear(16, 64)
+            self.blocks = torch.nn.ModuleList([torch.nn.Linear(64, 64) for _ in range(5)])
+            self.head = torch.nn.Linear(64, 3)
+
+        def forward(self, x):
+            x = self.emb(x)
+            for b in self.blocks:
+                x = torch.tanh(b(x))
+            return self.head(x)
+
+    torch.manual_seed(0)
+    ref = Toy().to(DEV)
+    x = torch.randn(32, 16, device=DEV)
+    for host in (False, True):
+        a, b = Toy().to(DEV), Toy().to(DEV)
+        a.load_state_dict(ref.state_dict())
+        b.load_state_dict(ref.state_dict())
+        oa = AdamW(list(a.parameters()), lr=1e-2, state_on_host=host)
+        ob = AdamW(list(b.parameters()), lr=1e-2, state_on_host=host, overlap=True, ring_slots=2)
+        ob.attach(b)
+        assert ob.params[0] is b.emb.weight and ob.params[-1] is b.head.bias
+        for it in range(4):
+            la, lb = a(x).square().mean(), b(x).square().mean()   # b's forward waits per block
+            assert torch.equal(la, lb), (host, it)
+            la.backward()
+            lb.backward()
+            oa.step()
+            ob.step()
+            assert len(ob._ready) == len(ob.params)
+            oa.zero_grad()
+            ob.zero_grad()
+        ob.synchronize()
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            assert torch.equal(pa, pb), host
+
+
 def test_sumsq_scale(ops):
     x = torch.randn(100003, device=DEV)
     out = torch.zeros(1, device=DEV)
