@@ -106,6 +106,19 @@ def cpu_baseline(L_sample=4096):
     return dt, flops, threads
 
 
+def pmc_traffic(L):
+    """HBM-side bytes per launch of the roofline kernel from the committed rocprofv3 --pmc passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/r01_pmc_attn_fwd720.txt, measured on
+    the isolated 720p self-attention forward).  PMC counters cannot be read inside this process."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_attn_fwd720.txt")
+    if L != 73920 or not os.path.exists(path):
+        return None, None
+    for line in open(path):
+        if line.startswith("HBM-side traffic per launch"):
+            return float(line.rsplit("=", 1)[1].split()[0]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def heartbeat(period=60.0):
     """A progress line on stderr every `period` s (a 720p iteration runs for minutes)."""
     import threading
@@ -208,6 +221,7 @@ def main():
     dom = "attn_fwd"
     d = prof[dom]
     achieved = d["work"] / (d["ms"] * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(L)
     value = world * args.steps / dt
     res = {
         "metric": "PRFL train steps/sec (whole node) + peak HBM GB, 14B DiT",
@@ -227,7 +241,9 @@ def main():
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "launches": d["count"], "avg_launch_ms": round(d["ms"] / d["count"], 3),
                      "work_per_launch_tflop": round(d["work"] / d["count"] / 1e12, 3),
-                     "traffic": None},
+                     "traffic": traffic, "traffic_unit": "GB HBM per launch (PMC)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_gb_per_launch": round(4 * L * C * 2 / 1e9, 3)},
         "kernels": {k: {"count": v["count"], "ms": round(v["ms"], 1),
                         "rate": round(v["work"] / (v["ms"] * 1e-3) / (1e9 if k in ("ln", "rms", "eltwise", "adamw") else 1e12), 1)}
                     for k, v in prof.items() if v["count"]},
