@@ -568,7 +568,7 @@ __device__ __forceinline__ float xhalf_max(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-template <bool SHORT_KV>
+template <bool SHORT_KV, int SCHED>
 __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[3 * 32768];   // ring of [K | V] tiles
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
@@ -672,6 +672,15 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
         for (int ks = 1; ks < 8; ++ks)
           s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
       }
+      if (SCHED) {   // K-row reads SCHED+1 MFMAs ahead, one per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 1, 0);
+#pragma unroll
+        for (int i = 0; i < 15 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
+      }
     }
     if (t > 0) {
       const char* Vs = smem + stp * 32768;
@@ -685,6 +694,15 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
             const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
             o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
           }
+      }
+      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
+#pragma unroll
+        for (int i = 0; i < 15 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1383,11 +1401,17 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   prfl_prof::begin(kid, s);
   static const int impl = getenv("PRFL_ATTN_FWD16") ? 16 : getenv("PRFL_ATTN_FWD32") ? 32
                           : getenv("PRFL_ATTN_PP1") ? 2 : 3;
-  if (impl == 3) {
-    if (kid == KID_ATTN_FWD)
-      hipLaunchKernelGGL(attn_fwd_pp2_kernel<false>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL(attn_fwd_pp2_kernel<true>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
+  static const int sched = getenv("PRFL_ATTN_SCHED") ? atoi(getenv("PRFL_ATTN_SCHED")) : 1;
+  const dim3 g2((Lq + 255) / 256, H, B);
+  if (impl == 3 && sched == 1) {
+    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 1>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 1>), g2, dim3(512), 0, s, a);
+  } else if (impl == 3 && sched == 3) {
+    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 3>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 3>), g2, dim3(512), 0, s, a);
+  } else if (impl == 3) {
+    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 0>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 0>), g2, dim3(512), 0, s, a);
   } else if (impl == 2) {
     if (kid == KID_ATTN_FWD)
       hipLaunchKernelGGL(attn_fwd_pp_kernel<false>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
