@@ -37,6 +37,21 @@ if which in ("attn", "attn_bwd"):
     for kname, d in ops.prof_collect().items():
         if d["count"]:
             print(f"  {kname}: {d['ms']:.2f} ms  {d['work'] / (d['ms'] * 1e-3) / 1e12:.0f} TF/s", flush=True)
+elif which == "gemmfwd":
+    # the forward projections of one block at L tokens (the rollout's hot GEMMs), bf16 epilogue
+    for (N, K, name) in [(3 * C, C, "qkv"), (C, C, "o/cq/co"), (F, C, "ffn1"), (C, F, "ffn2")]:
+        x = torch.randn(L, K, device=dev, generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        y = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, w, out=y)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for i in range(reps):
+            ops.linear(x, w, out=y)
+        torch.cuda.synchronize()
+        dt = (time.time() - t0) / reps
+        print(f"gemm {name} {L}x{N}x{K} {dt*1e3:.2f} ms  {2*L*N*K/dt/1e12:.0f} TF/s", flush=True)
+        del x, w, y
 else:
     x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(F, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
