@@ -32,6 +32,7 @@ struct AttnArgs {
   int Lq, Lk, H, k_len;
   float sl2;             // softmax_scale * log2(e)
   int stagger;           // attn_fwd32: waves 4-7 run one phase behind waves 0-3
+  unsigned long long* stamps;   // diagnostic build only (prfl_attn_fwd_stamped), else null
 };
 
 struct AttnBwdArgs {
@@ -563,12 +564,21 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(AttnArgs a) {
 //    ds_bpermute round trip on the softmax critical path;
 //  * waves 4-7 (the younger, lagging half) run at s_setprio 1 (MI355X guide, two waves per SIMD,
 //    item 4).
+// diagnostic cycle stamp (MI355X guide, in-kernel stamps): one asm statement with its lgkmcnt(0)
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-template <bool SHORT_KV, int SCHED>
+template <bool SHORT_KV, int SCHED, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[3 * 32768];   // ring of [K | V] tiles
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
@@ -660,6 +670,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
   f32x16 s[2];
   bf16x8 pf[2][2];
   int st = 0, stp = 2;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, sx = 0, sxb = 0, sy = 0, syb = 0;
+  if (STAMP) t0 = stamp();
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
@@ -705,8 +717,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
+    if (STAMP) t1 = stamp();
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
+    if (STAMP) t2 = stamp();
     // ---------------- Y_t ----------------
     if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
     if (t < nkv) {
@@ -748,10 +762,20 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
                                 f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
       }
     }
+    if (STAMP) t3 = stamp();
     if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
+    if (STAMP) {
+      const unsigned long long t4 = stamp();
+      sx += t1 - t0; sxb += t2 - t1; sy += t3 - t2; syb += t4 - t3;
+      t0 = t4;
+    }
     stp = st;
     st = st == 2 ? 0 : st + 1;
+  }
+  if (STAMP && a.stamps && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 16 && lane == 0) {
+    unsigned long long* o = a.stamps + (blockIdx.x * 8 + w) * 4;
+    o[0] = sx; o[1] = sxb; o[2] = sy; o[3] = syb;
   }
   if (gp == 0) bar();
   lsum += __shfl_xor(lsum, 32, 64);
@@ -1501,7 +1525,7 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
     return (int)hipErrorInvalidValue;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f, getenv("PRFL_ATTN_STAGGER") ? 1 : 0};
+             scale * 1.4426950408889634f, getenv("PRFL_ATTN_STAGGER") ? 1 : 0, nullptr};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
@@ -1580,6 +1604,23 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                        dim3(512), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+// Diagnostic build of the self-attention forward (attn_fwd_pp2_kernel with cycle stamps): per wave
+// of workgroups (x < 16, head 0, batch 0), stamps[(x*8 + wave)*4 + {0..3}] = summed cycles of
+// {MFMA phase, barrier wait after it, softmax phase, barrier wait after it}.  Read the SHARES, not
+// the run time (the stamps' lgkmcnt(0) fences change the schedule).  Not used by the product path.
+extern "C" int prfl_attn_fwd_stamped(const void* q, int64_t ldq, const void* k, int64_t ldk,
+                                     const void* v, int64_t ldv, void* o, int64_t ldo, float* lse2,
+                                     int64_t L, int64_t H, float scale,
+                                     unsigned long long* stamps, void* stream) {
+  if (L < 4096 || H <= 0) return (int)hipErrorInvalidValue;
+  AttnArgs a{(const bf16*)q, ldq, 0, (const bf16*)k, ldk, 0, (const bf16*)v, ldv, 0, (bf16*)o, ldo,
+             0, lse2, (int)L, (int)L, (int)H, (int)L, scale * 1.4426950408889634f, 0, stamps};
+  hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 1, true>), dim3((L + 255) / 256, H, 1), dim3(512),
+                     0, (hipStream_t)stream, a);
   PRFL_LAUNCH_CHECK();
   return 0;
 }

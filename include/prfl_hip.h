@@ -54,6 +54,11 @@ int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                   const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
                   float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
                   float scale, void* stream);
+/* Diagnostic only (not on the product path): the self-attention forward with in-kernel cycle
+ * stamps of its two phases and barrier waits, for tools/attn_stamps.py. */
+int prfl_attn_fwd_stamped(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                          int64_t ldv, void* o, int64_t ldo, float* lse2, int64_t L, int64_t H,
+                          float scale, unsigned long long* stamps, void* stream);
 /* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
  * caller-owned workspace. */
 int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
