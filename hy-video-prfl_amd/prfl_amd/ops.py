@@ -8,7 +8,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import I32, I64, F32, call, ptr, stream_ptr
+from ._lib import F32, I32, I64, P, call, ptr, stream_ptr
 
 BF16 = torch.bfloat16
 EPI_BF16, EPI_GELU, EPI_RESID, EPI_F32, EPI_DGELU = range(5)
@@ -236,3 +236,72 @@ def prof_collect():
     call("prfl_prof_collect", ctypes.cast(counts, ctypes.c_void_p), ctypes.cast(ms, ctypes.c_void_p),
          ctypes.cast(work, ctypes.c_void_p), I32(n))
     return {k: dict(count=counts[i], ms=ms[i], work=work[i]) for k, i in _lib.KID.items()}
+
+
+def _coef_array(coef):
+    import ctypes
+    assert len(coef) == 11
+    return (ctypes.c_float * 11)(*[float(c) for c in coef])
+
+
+def unipc_step_fwd(sample, model_output, last_sample, hist1, hist2, coef, corr_order, pred_order):
+    """Fused FlowUniPC update (csrc/unipc.hip).  Returns (m_t fp32, sample_c bf16, prev bf16)."""
+    import ctypes
+    _lib.require_gpu(sample, model_output)
+    if sample.dtype != torch.bfloat16 or model_output.dtype != torch.float32:
+        raise NotImplementedError("fused UniPC step: bf16 sample and fp32 model output "
+                                  "(the PRFL chain's dtypes, train_prfl.py:687-734)")
+    n = sample.numel()
+    for t in (model_output, last_sample, hist1, hist2):
+        if t is not None and (t.numel() != n or not t.is_contiguous()):
+            raise ValueError("fused UniPC step: operands must be contiguous with the sample's shape")
+    sample = sample.contiguous()
+    m_t = torch.empty(sample.shape, dtype=torch.float32, device=sample.device)
+    prev = torch.empty_like(sample)
+    sample_c = torch.empty_like(sample) if corr_order else sample
+    cf = _coef_array(coef)
+    call("prfl_unipc_step", ptr(sample), ptr(model_output), ptr(last_sample), ptr(hist1),
+         ptr(hist2), ptr(m_t), ptr(sample_c) if corr_order else P(0), ptr(prev), I64(n),
+         ctypes.cast(cf, ctypes.c_void_p), I32(corr_order), I32(pred_order), stream_ptr())
+    return m_t, sample_c, prev
+
+
+def unipc_step_bwd(grad_prev, coef, corr_order, pred_order):
+    import ctypes
+    g = grad_prev.to(torch.bfloat16).contiguous()
+    out = torch.empty(g.shape, dtype=torch.float32, device=g.device)
+    cf = _coef_array(coef)
+    call("prfl_unipc_step_bwd", ptr(g), ptr(out), I64(g.numel()), ctypes.cast(cf, ctypes.c_void_p),
+         I32(corr_order), I32(pred_order), stream_ptr())
+    return out
+
+
+class UniPCStep(torch.autograd.Function):
+    """Differentiable w.r.t. model_output only — the one input that carries the reward
+    gradient at train_prfl.py:734 (the sample comes out of the no-grad rollout)."""
+
+    @staticmethod
+    def forward(ctx, model_output, sample, last_sample, hist1, hist2, coef, corr_order, pred_order):
+        ctx.coef, ctx.corr, ctx.pred = coef, corr_order, pred_order
+        ctx.set_materialize_grads(False)
+        m_t, sample_c, prev = unipc_step_fwd(sample, model_output, last_sample, hist1, hist2, coef,
+                                             corr_order, pred_order)
+        ctx.mark_non_differentiable(sample_c)
+        return m_t, sample_c, prev
+
+    @staticmethod
+    def backward(ctx, g_mt, g_sc, g_prev):
+        if g_mt is not None:
+            raise NotImplementedError("fused UniPC step: gradient through the stored m_t history")
+        gmo = None
+        if g_prev is not None:
+            gmo = unipc_step_bwd(g_prev, ctx.coef, ctx.corr, ctx.pred)
+        return gmo, None, None, None, None, None, None, None
+
+
+def unipc_step(model_output, sample, last_sample, hist1, hist2, coef, corr_order, pred_order):
+    for t in (sample, last_sample, hist1, hist2):
+        if t is not None and t.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("fused UniPC step differentiates w.r.t. model_output only")
+    return UniPCStep.apply(model_output, sample, last_sample, hist1, hist2, coef, corr_order,
+                           pred_order)

@@ -2,10 +2,11 @@
 
 * FlowUniPCMultistepScheduler — bh2 UniPC, order 2, x0-prediction, as configured by
   `train_prfl.py:413-415, :633` (`wan/utils/fm_solvers_unipc.py`, itself diffusers v0.31.0's UniPC
-  adapted to flow matching).  The reward gradient flows through one `step` (`train_prfl.py:734`),
-  so every update here is plain differentiable tensor arithmetic with the reference's dtype
-  behaviour: the sample stays in its own dtype (bf16 in PRFL) and scalar coefficients are 0-dim
-  fp32 tensors, so `sigma_t/sigma_s0 * x` is rounded to bf16 exactly as in the reference.
+  adapted to flow matching).  The host computes the step's scalar coefficients exactly as the
+  reference does (0-dim fp32 tensors, rhos cast to bf16); the element-wise body — model-output
+  conversion, UniC corrector and UniP predictor — is ONE fused HIP kernel (`ops.unipc_step`,
+  csrc/unipc.hip), bit-identical to the reference's torch chain and differentiable w.r.t. the
+  model output, through which the reward gradient flows (`train_prfl.py:734`).
 * FlowMatchDiscreteScheduler — training-time sigma/timestep sampling, add_noise, target
   (`schedulers/scheduling_flow_match_discrete.py`).
 """
@@ -13,6 +14,8 @@ from types import SimpleNamespace
 
 import numpy as np
 import torch
+
+from . import ops
 
 
 class FlowUniPCMultistepScheduler:
@@ -85,60 +88,61 @@ class FlowUniPCMultistepScheduler:
         idx = (self.timesteps == t).nonzero()
         self._step_index = idx[1 if len(idx) > 1 else 0].item()
 
-    def _corrector(self, m_t, x_t):
-        """UniC-p (fm_solvers_unipc.py:486-626)."""
+    def _corrector_coef(self):
+        """UniC-p scalars (fm_solvers_unipc.py:486-626) as the reference computes them: 0-dim
+        fp32 host tensors; the solved rhos are cast to the sample dtype (bf16, :612)."""
         i, order = self._step_index, self.this_order
-        m0, x = self.model_outputs[-1], self.last_sample
         sig_t, sig_s0 = self.sigmas[i], self.sigmas[i - 1]
         alpha_t, h, hh, h_phi_1, B_h = self._coeffs(sig_t, sig_s0)
-        x_t_ = sig_t / sig_s0 * x - alpha_t * h_phi_1 * m0
+        r, c1, aBh = sig_t / sig_s0, alpha_t * h_phi_1, alpha_t * B_h
         if order == 1:
-            rho_last = torch.tensor(0.5, dtype=x.dtype)
-            corr = 0
-        else:
-            rk = (self._lambda(self.sigmas[i - 2]) - self._lambda(sig_s0)) / h
-            D1 = (self.model_outputs[-2] - m0) / rk
-            hpk = h_phi_1 / hh - 1
-            b1 = hpk / B_h
-            b2 = (hpk / hh - 0.5) * 2 / B_h
-            R = torch.stack([torch.stack([torch.ones(()), torch.ones(())]),
-                             torch.stack([rk, torch.ones(())])])
-            rhos = torch.linalg.solve(R, torch.stack([b1, b2])).to(x.dtype)
-            corr = rhos[0] * D1
-            rho_last = rhos[-1]
-        return (x_t_ - alpha_t * B_h * (corr + rho_last * (m_t - m0))).to(x.dtype)
+            return [r, c1, 1.0, 0.0, torch.tensor(0.5, dtype=torch.bfloat16), aBh], 1
+        rk = (self._lambda(self.sigmas[i - 2]) - self._lambda(sig_s0)) / h
+        hpk = h_phi_1 / hh - 1
+        b1 = hpk / B_h
+        b2 = (hpk / hh - 0.5) * 2 / B_h
+        R = torch.stack([torch.stack([torch.ones(()), torch.ones(())]),
+                         torch.stack([rk, torch.ones(())])])
+        rhos = torch.linalg.solve(R, torch.stack([b1, b2])).to(torch.bfloat16)
+        return [r, c1, rk, rhos[0], rhos[-1], aBh], 2
 
-    def _predictor(self, x):
-        """UniP-p (fm_solvers_unipc.py:350-484)."""
-        i, m0 = self._step_index, self.model_outputs[-1]
+    def _predictor_coef(self):
+        """UniP-p scalars (fm_solvers_unipc.py:350-484)."""
+        i = self._step_index
         sig_t, sig_s0 = self.sigmas[i + 1], self.sigmas[i]
         alpha_t, h, hh, h_phi_1, B_h = self._coeffs(sig_t, sig_s0)
-        x_t_ = sig_t / sig_s0 * x - alpha_t * h_phi_1 * m0
+        rk = 1.0
         if self.this_order == 2:
             rk = (self._lambda(self.sigmas[i - 1]) - self._lambda(sig_s0)) / h
-            D1 = (self.model_outputs[-2] - m0) / rk
-            x_t_ = x_t_ - alpha_t * B_h * (torch.tensor(0.5, dtype=x.dtype) * D1)
-        return x_t_.to(x.dtype)
+        return [sig_t / sig_s0, alpha_t * h_phi_1, rk, alpha_t * B_h], self.this_order
+
+    # the fused element-wise update (csrc/unipc.hip); tests swap in the oracle's restatement
+    _update = staticmethod(ops.unipc_step)
 
     def step(self, model_output, timestep, sample, return_dict=True, generator=None):
         if self.num_inference_steps is None:
             raise ValueError("call set_timesteps first")
         if self._step_index is None:
             self._init_step_index(timestep)
-        # sigmas stay on the host as 0-dim fp32 scalars (as in the reference): scalar x device
-        # tensor keeps the sample dtype and needs no host<->device traffic
         i = self._step_index
-        m_t = sample - self.sigmas[i] * model_output                # convert_model_output (:321)
+        corr_c, corr = [0.0] * 6, 0
         if i > 0 and (i - 1) not in self.disable_corrector and self.last_sample is not None:
-            sample = self._corrector(m_t, sample)
-        self.model_outputs = self.model_outputs[1:] + [m_t]
-        self.timestep_list = self.timestep_list[1:] + [timestep]
+            corr_c, corr = self._corrector_coef()
         order = self.config.solver_order
         if self.config.lower_order_final:
             order = min(order, len(self.timesteps) - i)
-        self.this_order = min(order, self.lower_order_nums + 1)
-        self.last_sample = sample
-        prev = self._predictor(sample)
+        this_order = min(order, self.lower_order_nums + 1)
+        self.this_order = this_order
+        pred_c, pred = self._predictor_coef()
+        coef = [float(c) for c in [self.sigmas[i]] + corr_c + pred_c]
+        h1, h2 = self.model_outputs[-1], self.model_outputs[-2]
+        m_t, sample_c, prev = self._update(model_output, sample,
+                                           self.last_sample if corr else None,
+                                           h1 if (corr or pred == 2) else None,
+                                           h2 if corr == 2 else None, coef, corr, pred)
+        self.model_outputs = self.model_outputs[1:] + [m_t]
+        self.timestep_list = self.timestep_list[1:] + [timestep]
+        self.last_sample = sample_c
         self.lower_order_nums = min(self.lower_order_nums + 1, self.config.solver_order)
         self._step_index += 1
         return (prev,) if not return_dict else SimpleNamespace(prev_sample=prev)

@@ -115,6 +115,27 @@ int prfl_scale(float* x, int64_t n, const float* factor, void* stream);
 int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, void* stream);
 
+/* ---- FlowUniPC sampler update (bh2, order <= 2, x0-prediction) ----------------------------
+ * Replaces the element-wise body of FlowUniPCMultistepScheduler.step
+ * (diffusers_lite/wan/utils/fm_solvers_unipc.py:655-739: convert_model_output :321, UniC
+ * corrector :486-626, UniP predictor :350-484), called from train_prfl.py:693 (no-grad rollout)
+ * and :734 (the differentiable step the reward gradient flows through).
+ * sample / last_sample / sample_c / prev are bf16, model_output / hist1 (= model_outputs[-1]) /
+ * hist2 (= model_outputs[-2]) / m_t are fp32, all n contiguous elements.
+ * coef[11] (host) = {sigma_i, corrector: sig_t/sig_s0, alpha_t*h_phi_1, rk, rho0, rho_last,
+ *                    alpha_t*B_h, predictor: sig_t/sig_s0, alpha_t*h_phi_1, rk, alpha_t*B_h}
+ * with rho0/rho_last already rounded to bf16 (the reference casts the solved rhos, :612).
+ * corr_order 0 = no corrector (then last_sample/hist2 may be NULL, sample_c optional).
+ * Bit-identical to the reference's torch chain (fp32 ops in its order, no FMA contraction). */
+int prfl_unipc_step(const void* sample, const float* model_output, const void* last_sample,
+                    const float* hist1, const float* hist2, float* m_t, void* sample_c,
+                    void* prev, int64_t n, const float* coef, int corr_order, int pred_order,
+                    void* stream);
+/* d prev (bf16) -> d model_output (fp32): the transpose of the map above as torch autograd
+ * evaluates it (model_output is the only differentiable input, as in train_prfl.py:734). */
+int prfl_unipc_step_bwd(const void* grad_prev, float* grad_model_output, int64_t n,
+                        const float* coef, int corr_order, int pred_order, void* stream);
+
 /* ---- profiling (bench.py roofline) -------------------------------------------------------- */
 int prfl_prof_enable(int on);
 int prfl_prof_collect(int64_t* counts, double* ms, double* work, int nkid);

@@ -64,10 +64,14 @@ def test_import_shim():
 
 
 def test_unipc_product_vs_reference(golden):
-    """The product scheduler is host logic over device tensors; run it on CPU tensors here."""
+    """The product scheduler's host logic (step bookkeeping + scalar coefficients) with the
+    oracle's restatement of the element-wise body standing in for the fused HIP kernel (which
+    tests/test_gpu_kernels.py checks bit-exact against the same golden trajectory)."""
+    from oracle.wan_oracle import unipc_update
     from prfl_amd.schedulers import FlowUniPCMultistepScheduler
     g = golden("schedulers")
     sch = FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1, use_dynamic_shifting=False)
+    sch._update = unipc_update
     sch.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
     assert np.array_equal(sch.timesteps.numpy(), g["unipc_timesteps"])
     assert np.array_equal(sch.sigmas.numpy(), g["unipc_sigmas"])
