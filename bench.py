@@ -1,6 +1,7 @@
 """PRFL training-step benchmark (BASELINE.json metric) on 1..8 MI355X, one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload prfl_t2v_720|prfl_t2v_480|pavrm_t2v_480]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--workload prfl_t2v_720|prfl_t2v_480|prfl_i2v_720|pavrm_t2v_480]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Workload (default): `configs/train_prfl_t2v_720.yaml` — the metric's 720p x 81f configuration
@@ -11,7 +12,9 @@ through all of it, clip, AdamW every 5th micro-step; the timed window ends on an
 on the 14B Wan2.1 T2V DiT (40 blocks, C=5120), random-init weights (head perturbed so gradients
 are non-zero), synthetic latents/text.  Memory plan: on one GPU the AdamW moments
 live in pinned host memory and stream through HBM during the step; with N ranks they are
-ZeRO-1 sharded across the GPUs.  `--workload prfl_t2v_480` runs the 480p x 81f config (L=32760).
+ZeRO-1 sharded across the GPUs.  `--workload prfl_t2v_480` runs the 480p x 81f config (L=32760);
+`--workload prfl_i2v_720` the I2V model (16.4B, 36 input channels, 257 CLIP tokens of image
+cross-attention, `configs/train_prfl_i2v_720.yaml`) at 720p x 81f.
 
 Multi-GPU: pure data parallel (weak scaling, one sample per rank), RCCL all-reduce of the
 generator gradients overlapped with the backward (prfl_amd/dist.py).  `value` = PRFL sample-
@@ -37,15 +40,22 @@ PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-def block_fwd_flops(L, Lctx=TXT):
-    """8LC^2 + 4L^2C + 4LC^2 + 4 Lctx C^2 + 4 L Lctx C + 4LCF."""
-    return 8 * L * C * C + 4 * L * L * C + 4 * L * C * C + 4 * Lctx * C * C + 4 * L * Lctx * C + 4 * L * C * F
+CLIP_TOK = 257
 
 
-def iteration_flops(L, mid):
+def block_fwd_flops(L, Lctx=TXT, i2v=False):
+    """8LC^2 + 4L^2C + 4LC^2 + 4 Lctx C^2 + 4 L Lctx C + 4LCF; I2V adds the image
+    cross-attention 4*257*C^2 + 4*L*257*C (k_img/v_img projections + attention)."""
+    f = 8 * L * C * C + 4 * L * L * C + 4 * L * C * C + 4 * Lctx * C * C + 4 * L * Lctx * C + 4 * L * C * F
+    if i2v:
+        f += 4 * CLIP_TOK * C * C + 4 * L * CLIP_TOK * C
+    return f
+
+
+def iteration_flops(L, mid, i2v=False):
     """Algorithmic FLOPs of one PRFL iteration (no recompute): SFT 3G + reward (mid+1)G+2G+3R."""
-    G = NL * block_fwd_flops(L)
-    R = 8 * block_fwd_flops(L)
+    G = NL * block_fwd_flops(L, i2v=i2v)
+    R = 8 * block_fwd_flops(L, i2v=i2v)
     return 3 * G + (mid + 1) * G + 2 * G + 3 * R
 
 
@@ -60,16 +70,17 @@ def setup():
     return world, rank, local
 
 
-def build_models(dev, seed):
+def build_models(dev, seed, model_type="t2v"):
     from prfl_amd.model import WanModel
     from prfl_amd.network import MLP, QueryAttention
     torch.manual_seed(seed)
+    in_dim = 16 if model_type == "t2v" else 36   # I2V: 16 latent + 4 mask + 16 condition channels
     with torch.device(dev):
-        gen = WanModel(model_type="t2v", dim=C, ffn_dim=F, freq_dim=256, text_dim=4096, out_dim=16,
-                       num_heads=NH, num_layers=NL, in_dim=16)
+        gen = WanModel(model_type=model_type, dim=C, ffn_dim=F, freq_dim=256, text_dim=4096,
+                       out_dim=16, num_heads=NH, num_layers=NL, in_dim=in_dim)
         torch.nn.init.normal_(gen.head.head.weight, std=0.02)   # random-init trap
-        lrm = WanModel(model_type="t2v", dim=C, ffn_dim=F, freq_dim=256, text_dim=4096, out_dim=16,
-                       num_heads=NH, num_layers=8, in_dim=16)    # == blocks[0:8] of the base model
+        lrm = WanModel(model_type=model_type, dim=C, ffn_dim=F, freq_dim=256, text_dim=4096,
+                       out_dim=16, num_heads=NH, num_layers=8, in_dim=in_dim)   # == blocks[0:8]
         del lrm.head
         lrm.head = None
         qa = QueryAttention(C, 1, 8, 0., return_type="query")
@@ -137,7 +148,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="prfl_t2v_720",
-                    choices=["prfl_t2v_480", "prfl_t2v_720", "pavrm_t2v_480"])
+                    choices=["prfl_t2v_480", "prfl_t2v_720", "prfl_i2v_720", "pavrm_t2v_480"])
     ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -151,10 +162,20 @@ def main():
     # latents (gen_wanx_latent.py:117-149): 480p x 81f [16,21,60,104]; 720p x 81f [16,21,88,160]
     Fl, Hl, Wl = (21, 88, 160) if args.workload.endswith("720") else (21, 60, 104)
     L = Fl * (Hl // 2) * (Wl // 2)
-    gen, lrm, qa, mlp = build_models(dev, 110221)
+    i2v = "_i2v_" in args.workload
+    gen, lrm, qa, mlp = build_models(dev, 110221, "i2v" if i2v else "t2v")
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
+    clip, cond = None, None
+    if i2v:
+        # image condition as before_train_step builds it (train_prfl.py:531-549): CLIP tokens
+        # [1,257,1280]; condition latent [1,16,F,H,W] behind 4 mask channels (first frame = 1)
+        clip = torch.randn(1, CLIP_TOK, 1280, generator=g, device=dev).to(torch.bfloat16)
+        cond = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
+        mask = torch.zeros(1, 4, Fl, Hl, Wl, device=dev, dtype=torch.bfloat16)
+        mask[:, :, :1] = 1
+        cond = torch.cat([mask, cond], dim=1)
     if args.workload.startswith("prfl"):
         # 720p memory plan: the AdamW moments live in pinned host memory and stream
         # through HBM during the step; with DP ranks they are also ZeRO-1 sharded (each rank
@@ -166,10 +187,11 @@ def main():
                          optimizer_overlap=os.environ.get("PRFL_OPT_OVERLAP", "1") == "1")
 
         def one(step):
-            a = tr.sft_step(step, latents, text, L, generator=g)
-            b = tr.reward_step(step, latents, text, L, mid_timestep=args.mid, generator=g)
+            a = tr.sft_step(step, latents, text, L, image_embeds=clip, cond=cond, generator=g)
+            b = tr.reward_step(step, latents, text, L, image_embeds=clip, cond=cond,
+                               mid_timestep=args.mid, generator=g)
             return a, b
-        flops_it = iteration_flops(L, args.mid)
+        flops_it = iteration_flops(L, args.mid, i2v)
     else:
         del gen
         for blk in lrm.blocks:
@@ -231,7 +253,8 @@ def main():
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents/text, random-init 14B weights",
         "config": {"workload": ("train_%s: SFT + reward step, mid_timestep=%d" % (args.workload, args.mid)
                                 if args.workload.startswith("prfl") else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
-                   "model": "Wan2.1-T2V-14B (40 blocks, C=5120)", "latent": [16, Fl, Hl, Wl],
+                   "model": ("Wan2.1-I2V-14B (40 blocks, C=5120, image cross-attn)" if i2v
+                             else "Wan2.1-T2V-14B (40 blocks, C=5120)"), "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
         "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),
         "algorithmic_tflop_per_step": round(flops_it / 1e12, 1),
