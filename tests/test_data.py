@@ -81,15 +81,20 @@ def test_prefetcher_stages_batches_like_reference(tmp_path):
     lst, null = DF.build(str(tmp_path))
     ds = Image2VideoTrainDataset(task="i2v-14b-720p", dataset_type="refl", meta_file_list=[lst],
                                  null_dir=null)
-    sampler = BlockDistributedSampler(list(range(5)), 1, 0, shuffle=True, seed=9)
-    ds.meta_paths = ds.meta_paths[:5]                      # skip the broken clip
-    order = list(iter(sampler))
+    # the clips the "refl" reader accepts (imgclip_path + a text pair or text_en_path)
+    ds.meta_paths = [ds.meta_paths[i] for i in (0, 2, 3)]
+    sampler = BlockDistributedSampler(list(range(3)), 1, 0, shuffle=True, seed=9)
+    order = []
+    for ep in range(3):                                    # the reader advances the epoch
+        s2 = BlockDistributedSampler(list(range(3)), 1, 0, shuffle=True, seed=9)
+        s2.set_epoch(ep)
+        order += list(iter(s2))
     random.seed(5)
     pf = LatentPrefetcher(ds, sampler, batch_size=1, device="cuda", task="i2v-14b-720p")
     try:
         for k in range(7):                                 # crosses an epoch boundary
             b = next(pf)
-            i = order[k % 5]
+            i = order[k]
             item = ds.get_batch_lrm_refl(i)
             ref_lat = item[0][None].to(torch.bfloat16)
             assert b.latents.dtype == torch.bfloat16 and b.latents.is_cuda
