@@ -14,7 +14,8 @@ are non-zero), synthetic latents/text.  Memory plan: on one GPU the 
 live in pinned host memory and stream through HBM during the step; with N ranks they are
 ZeRO-1 sharded across the GPUs.  `--workload prfl_t2v_480` runs the 480p x 81f config (L=32760);
 `--workload prfl_i2v_720` the I2V model (16.4B, 36 input channels, 257 CLIP tokens of image
-cross-attention, `configs/train_prfl_i2v_720.yaml`) at 720p x 81f.
+cross-attention, `configs/train_prfl_i2v_720.yaml`) at 720p x 81f; `--fp8` its fp8 path (C5: the
+large forward projections as per-row e4m3 on the block-scaled fp8 MFMA, backward bf16).
 
 Multi-GPU: pure data parallel (weak scaling, one sample per rank), RCCL all-reduce of the
 generator gradients overlapped with the backward (prfl_amd/dist.py).  `value` = PRFL sample-
@@ -151,6 +152,8 @@ def main():
                     choices=["prfl_t2v_480", "prfl_t2v_720", "prfl_i2v_720", "pavrm_t2v_480"])
     ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp8", action="store_true",
+                    help="config C5's fp8 path: e4m3 forward projections on the block-scaled MFMA")
     args = ap.parse_args()
     world, rank, local = setup()
     dev = torch.device("cuda", local)
@@ -164,6 +167,9 @@ def main():
     L = Fl * (Hl // 2) * (Wl // 2)
     i2v = "_i2v_" in args.workload
     gen, lrm, qa, mlp = build_models(dev, 110221, "i2v" if i2v else "t2v")
+    if args.fp8:
+        gen.set_fp8_gemm(True)
+        lrm.set_fp8_gemm(True)
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)
@@ -250,7 +256,8 @@ def main():
         "value": round(value, 6), "unit": "PRFL iterations/s (all ranks)",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents/text, random-init 14B weights",
+        "vs_baseline": None,
+        "dtype": "fp8-e4m3 fwd GEMMs / bf16" if args.fp8 else "bf16", "data": "synthetic latents/text, random-init 14B weights",
         "config": {"workload": ("train_%s: SFT + reward step, mid_timestep=%d" % (args.workload, args.mid)
                                 if args.workload.startswith("prfl") else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
                    "model": ("Wan2.1-I2V-14B (40 blocks, C=5120, image cross-attn)" if i2v

@@ -598,3 +598,219 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
   prfl_prof::end(KID_GEMM, s);
   return rc;
 }
+
+// ================================================================ fp8 (C5: I2V 720p fp8 path) ===
+// C[m][n] = sa[m] * sb[n] * sum_k A8(m,k) B8(n,k)   (+ the bf16 kernel's epilogues)
+// A8 / B8 are OCP e4m3 (gfx950 `e4m3fn`), both K-major, quantised per row (prfl_quant_rows_fp8).
+// The MFMA is the block-scaled `v_mfma_scale_f32_16x16x128_f8f6f4` (2x the bf16 MFMA rate; the
+// unscaled fp8 forms run at the bf16 rate) with every E8M0 block scale = 2^0: the per-row /
+// per-column dequantisation happens once, in fp32, in the epilogue.
+// Same 256x256 tile, 8-wave grid and 2-deep LDS-DMA ring as gemm256_kernel; BK = 128 fp8 = 128 B
+// per row, so the swizzled LDS image (128-B rows, 16-B chunk ^ (row & 7)) is byte-identical to
+// the bf16 kernel's; each lane's fragment is 32 consecutive k (two 16-B chunks).
+namespace {
+constexpr int BK8 = 128;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+struct ScaleArgs {
+  const float* sa;   // [M]
+  const float* sb;   // [N]
+};
+
+__device__ __forceinline__ void dma_tile8(char* lds, const uint8_t* __restrict__ P, int64_t ld,
+                                          int rows, int r0, int k0, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wid * 4 + i;                     // 32 pieces of 1 KiB = 8 rows x 128 B
+    const int row = piece * 8 + (lane >> 3), pc = lane & 7;
+    const int gr = min(r0 + row, rows - 1);
+    dma16(P + (int64_t)gr * ld + k0 + ((pc ^ (row & 7)) << 4), lds_addr(lds + piece * 1024));
+  }
+}
+
+// lane l: X[row = base + (l&15)][k = 32*(l>>4) + 0..31] (chunks 2g, 2g+1 of the 128-B row)
+__device__ __forceinline__ i32x8 read_frag8(const char* lds, int base, int lane) {
+  const int row = base + (lane & 15);
+  const int c0 = 2 * (lane >> 4);
+  const u32x4 lo = *(const u32x4*)(lds + row * 128 + ((c0 ^ (row & 7)) << 4));
+  const u32x4 hi = *(const u32x4*)(lds + row * 128 + (((c0 + 1) ^ (row & 7)) << 4));
+  return (i32x8){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3],
+                 (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
+__device__ __forceinline__ f32x4 mfma_fp8(i32x8 a, i32x8 b, f32x4 c) {
+  // cbsz = blgp = 0: both operands e4m3; opsel 0 picks byte 0 of the scale words: 127 = 2^0
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0,
+                                                          0x7f7f7f7f);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT2, 1) void gemm256_fp8_kernel(GemmArgs g, ScaleArgs sc) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A|B], 32 KiB each
+  int tm, tn;
+  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const uint8_t* A = (const uint8_t*)g.A;
+  const uint8_t* B = (const uint8_t*)g.B;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK8;
+  dma_tile8(smem, A, g.lda, g.M, m0, 0, wid, lane);
+  dma_tile8(smem + TILE2, B, g.ldb, g.N, n0, 0, wid, lane);
+  if (nk > 1) {
+    dma_tile8(smem + 2 * TILE2, A, g.lda, g.M, m0, BK8, wid, lane);
+    dma_tile8(smem + 3 * TILE2, B, g.ldb, g.N, n0, BK8, wid, lane);
+  }
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* As = smem + (t & 1) * 2 * TILE2;
+    const char* Bs = As + TILE2;
+    i32x8 bf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = read_frag8(Bs, wc * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const i32x8 af = read_frag8(As, wr * 128 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_fp8(bf[j], af, acc[i][j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) {
+      char* st = smem + (t & 1) * 2 * TILE2;
+      dma_tile8(st, A, g.lda, g.M, m0, (t + 2) * BK8, wid, lane);
+      dma_tile8(st + TILE2, B, g.ldb, g.N, n0, (t + 2) * BK8, wid, lane);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const float s_m = sc.sa[m];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      const f32x4 s_n = *(const f32x4*)(sc.sb + n);
+      f32x4 v = acc[i][j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] * (s_m * s_n[r]);
+      epilogue_tile<true, true, EPI>(g, v, m, n);
+    }
+  }
+}
+
+// ---- per-row e4m3 quantisation: scale[m] = amax_m / 448, q = e4m3(x * (448 / amax_m)) ------
+constexpr int QNT = 256, QMAXC = 8;     // <= 8 chunks of 8 per thread: K <= 16384
+constexpr float E4M3_MAX = 448.f;
+
+__device__ __forceinline__ float ldf(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float ldf(const bf16* p, int64_t i) { return bf2f(p[i]); }
+
+template <typename T>
+__global__ __launch_bounds__(QNT) void quant_rows_fp8_kernel(const T* __restrict__ x, int64_t ldx,
+                                                             int K, uint8_t* __restrict__ q,
+                                                             int64_t ldq,
+                                                             float* __restrict__ scale) {
+  __shared__ float red[QNT / 64];
+  const int64_t m = blockIdx.x;
+  const T* xr = x + m * ldx;
+  const int nch = K / 8;
+  float v[QMAXC][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < QMAXC; ++c) {
+    const int ch = threadIdx.x + c * QNT;
+    if (ch < nch) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v[c][r] = ldf(xr, (int64_t)ch * 8 + r);
+        amax = fmaxf(amax, fabsf(v[c][r]));
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float inv = amax > 0.f ? E4M3_MAX / amax : 1.f;
+  if (threadIdx.x == 0) scale[m] = amax > 0.f ? amax / E4M3_MAX : 1.f;
+  uint8_t* qr = q + m * ldq;
+#pragma unroll
+  for (int c = 0; c < QMAXC; ++c) {
+    const int ch = threadIdx.x + c * QNT;
+    if (ch < nch) {
+      int lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * inv, v[c][1] * inv, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * inv, v[c][3] * inv, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4] * inv, v[c][5] * inv, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][6] * inv, v[c][7] * inv, hi, true);
+      *(uint2*)(qr + (int64_t)ch * 8) = make_uint2((unsigned)lo, (unsigned)hi);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int prfl_quant_rows_fp8(const void* x, int x_f32, int64_t ldx, int64_t M, int64_t K,
+                                   void* q, int64_t ldq, float* scale, void* stream) {
+  if (M <= 0) return 0;
+  if (K <= 0 || K % 8 || K > 8LL * QNT * QMAXC || ldx % 8 || ldq % 8 || M > 0x7fffffff)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  prfl_prof::begin(KID_ELTWISE, s);
+  if (x_f32)
+    hipLaunchKernelGGL(quant_rows_fp8_kernel<float>, dim3(M), dim3(QNT), 0, s, (const float*)x,
+                       ldx, (int)K, (uint8_t*)q, ldq, scale);
+  else
+    hipLaunchKernelGGL(quant_rows_fp8_kernel<bf16>, dim3(M), dim3(QNT), 0, s, (const bf16*)x,
+                       ldx, (int)K, (uint8_t*)q, ldq, scale);
+  prfl_prof::set_work((double)M * K * ((x_f32 ? 4 : 2) + 1));
+  prfl_prof::end(KID_ELTWISE, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const void* B,
+                             int64_t ldb, const float* sb, void* C, int64_t ldc, int64_t M,
+                             int64_t N, int64_t K, int epilogue, const void* bias,
+                             const float* gate, const void* res, int64_t ldr, int res_bf16,
+                             void* aux, int64_t ldaux, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || K % BK8 || N % 4 || lda % 16 || ldb % 16 || ((uintptr_t)A & 15) ||
+      ((uintptr_t)B & 15) || ((uintptr_t)sb & 15) || !sa || !sb)
+    return (int)hipErrorInvalidValue;
+  if (M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) return (int)hipErrorInvalidValue;
+  if (epilogue != EPI_BF16 && epilogue != EPI_GELU && epilogue != EPI_RESID)
+    return (int)hipErrorInvalidValue;
+  GemmArgs g{(const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, (int)M, (int)N, (int)K,
+             (const bf16*)bias, gate, res, ldr, res_bf16, (bf16*)aux, ldaux, 0};
+  ScaleArgs sc{sa, sb};
+  hipStream_t s = (hipStream_t)stream;
+  const int nt = (int)(((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2));
+  prfl_prof::begin(KID_GEMM, s);
+  if (epilogue == EPI_BF16)
+    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_BF16>, dim3(nt), dim3(NT2), 0, s, g, sc);
+  else if (epilogue == EPI_GELU)
+    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_GELU>, dim3(nt), dim3(NT2), 0, s, g, sc);
+  else
+    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_RESID>, dim3(nt), dim3(NT2), 0, s, g, sc);
+  prfl_prof::set_work(2.0 * (double)M * (double)N * (double)K);
+  prfl_prof::end(KID_GEMM, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}

@@ -37,8 +37,9 @@ def param_names(i2v):
 class Meta:
     """Non-tensor block arguments."""
 
-    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6):
+    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6, fp8=False):
         self.num_heads = num_heads
+        self.fp8 = fp8              # config C5: fp8 forward projections (WanModel.set_fp8_gemm)
         self.grid = grid            # list of (F, H, W) per sample
         self.seq_len = seq_len      # list of valid key lengths per sample (k_lens)
         self.rope_tab = rope_tab    # fp32 [1024, 64, 2] device tensor
@@ -47,26 +48,63 @@ class Meta:
 
 
 class BF16Weights:
-    """bf16 copies of a block's Linear weights/biases for one forward or backward pass."""
+    """bf16 copies of a block's Linear weights/biases for one forward or backward pass.
 
-    def __init__(self, P):
+    With ``fp8`` the six large forward projections (QKV, O, cross q/o, FFN in/out) also get
+    per-output-row e4m3 copies quantised straight from the fp32 masters (``self.q[name]`` =
+    (codes, scales)); ``need_bf16=False`` (a no-grad forward on the fp8 path) skips their bf16
+    casts — only the backward's dX GEMMs read those."""
+
+    FP8_KEYS = {"qkv": None, "o": "self_attn.o", "cq": "cross_attn.q", "co": "cross_attn.o",
+                "1": "ffn.0", "2": "ffn.2"}
+
+    def __init__(self, P, fp8=False, need_bf16=True):
         g = P.__getitem__
         C = g("self_attn.q.weight").shape[0]
         dev = g("self_attn.q.weight").device
-        self.wqkv = torch.empty(3 * C, C, dtype=BF16, device=dev)
+        self.fp8 = fp8
+        self.q = {}
+        big = need_bf16 or not fp8
+        if big:
+            self.wqkv = torch.empty(3 * C, C, dtype=BF16, device=dev)
         self.bqkv = torch.empty(3 * C, dtype=BF16, device=dev)
         for i, n in enumerate("qkv"):
-            ops.cast_bf16(g(f"self_attn.{n}.weight"), self.wqkv[i * C:(i + 1) * C])
+            if big:
+                ops.cast_bf16(g(f"self_attn.{n}.weight"), self.wqkv[i * C:(i + 1) * C])
             ops.cast_bf16(g(f"self_attn.{n}.bias"), self.bqkv[i * C:(i + 1) * C])
         c = lambda n: ops.cast_bf16(g(n))  # noqa: E731
-        self.wo, self.bo = c("self_attn.o.weight"), c("self_attn.o.bias")
+        cw = lambda n: c(n) if big else None  # noqa: E731
+        self.wo, self.bo = cw("self_attn.o.weight"), c("self_attn.o.bias")
         for n in ("q", "k", "v", "o", "k_img", "v_img"):
             key = f"cross_attn.{n}.weight"
             if key in P:
-                setattr(self, "wc" + n, c(key))
+                setattr(self, "wc" + n, cw(key) if n in ("q", "o") else c(key))
                 setattr(self, "bc" + n, c(f"cross_attn.{n}.bias"))
-        self.w1, self.b1 = c("ffn.0.weight"), c("ffn.0.bias")
-        self.w2, self.b2 = c("ffn.2.weight"), c("ffn.2.bias")
+        self.w1, self.b1 = cw("ffn.0.weight"), c("ffn.0.bias")
+        self.w2, self.b2 = cw("ffn.2.weight"), c("ffn.2.bias")
+        if fp8:
+            for name, pre in self.FP8_KEYS.items():
+                if pre is None:     # q/k/v rows quantised into one [3C, C] operand
+                    wq = torch.empty(3 * C, C, dtype=ops.FP8, device=dev)
+                    ws = torch.empty(3 * C, dtype=torch.float32, device=dev)
+                    for i, n in enumerate("qkv"):
+                        ops.quant_rows_fp8(g(f"self_attn.{n}.weight"), wq[i * C:(i + 1) * C],
+                                           ws[i * C:(i + 1) * C])
+                    self.q[name] = (wq, ws)
+                else:
+                    self.q[name] = ops.quant_rows_fp8(g(pre + ".weight"))
+
+
+def lin(W, name, x, **kw):
+    """The block's forward projection `name` (qkv, o, cq, co, 1, 2) of x [M, K] bf16: on the fp8
+    path x is quantised per row and the GEMM runs on the block-scaled fp8 MFMA, otherwise bf16."""
+    wn = {"qkv": "qkv", "o": "o", "cq": "cq", "co": "co", "1": "1", "2": "2"}[name]
+    bias = getattr(W, "b" + wn)
+    if W.fp8:
+        xq, xs = ops.quant_rows_fp8(x)
+        wq, ws = W.q[name]
+        return ops.linear_fp8(xq, xs, wq, ws, bias, **kw)
+    return ops.linear(x, getattr(W, "w" + wn), bias, **kw)
 
 
 def _split_ctx(ctx, i2v):
@@ -84,14 +122,14 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
     S = {}
     # ---- self-attention (model.py:344-348) ----
     h1, m1, r1 = ops.ln_mod_fwd(x, scale=e[1], shift=e[0], eps=eps)
-    qkv = ops.linear(h1, W.wqkv, W.bqkv)
+    qkv = lin(W, "qkv", h1)
     q_raw, k_raw, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     grid = meta.grid[b]
     qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid)
     kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
     ao, lse = ops.attn_fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
     y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
-    x1 = ops.linear(ao, W.wo, W.bo, EPI_RESID, gate=e[2], res=x, aux=y1)
+    x1 = lin(W, "o", ao, epilogue=EPI_RESID, gate=e[2], res=x, aux=y1)
     if save:
         S.update(h1=h1, m1=m1, r1=r1, qkv=qkv, qr=qr, rq=rq, kr=kr, rk=rk, ao=ao, lse=lse, y1=y1,
                  x1=x1)
@@ -99,7 +137,7 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
         del h1, qkv, qr, kr, ao
     # ---- cross-attention (model.py:352, :204-271) ----
     n3, m3, r3 = ops.ln_mod_fwd(x1, w=g("norm3.weight"), b=g("norm3.bias"), eps=eps)
-    qc_raw = ops.linear(n3, W.wcq, W.bcq)
+    qc_raw = lin(W, "cq", n3)
     qc, rqc = ops.rms_rope_fwd(qc_raw, g("cross_attn.norm_q.weight"), eps)
     ctx_t, ctx_i = _split_ctx(ctx, meta.i2v)
     kc_raw = ops.linear(ctx_t, W.wck, W.bck)
@@ -115,7 +153,7 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
     else:
         acs = ac
     x2 = x1 if not save else torch.empty_like(x1)
-    ops.linear(acs, W.wco, W.bco, EPI_RESID, out=x2, res=x1)
+    lin(W, "co", acs, epilogue=EPI_RESID, out=x2, res=x1)
     if save:
         S.update(n3=n3, m3=m3, r3=r3, qc_raw=qc_raw, qc=qc, rqc=rqc, kc_raw=kc_raw, kc=kc, rkc=rkc,
                  vc=vc, ac=ac, lsec=lsec, acs=acs, x2=x2)
@@ -124,10 +162,10 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
     # ---- FFN (model.py:353-355) ----
     h2, m2, r2 = ops.ln_mod_fwd(x2, scale=e[4], shift=e[3], eps=eps)
     fpre = torch.empty(L, W.w1.shape[0], dtype=BF16, device=x.device) if save else None
-    fact = ops.linear(h2, W.w1, W.b1, EPI_GELU, aux=fpre)
+    fact = lin(W, "1", h2, epilogue=EPI_GELU, aux=fpre)
     y2 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
     out = torch.empty_like(x2) if save else x2
-    ops.linear(fact, W.w2, W.b2, EPI_RESID, out=out, gate=e[5], res=x2, aux=y2)
+    lin(W, "2", fact, epilogue=EPI_RESID, out=out, gate=e[5], res=x2, aux=y2)
     if save:
         S.update(h2=h2, m2=m2, r2=r2, fpre=fpre, fact=fact, y2=y2)
     return out, S
@@ -257,7 +295,7 @@ class WanBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, x, e, context, meta, names, *params):
         P = dict(zip(names, params))
-        W = BF16Weights(P)
+        W = BF16Weights(P, fp8=meta.fp8, need_bf16=False)
         outs = []
         for b in range(x.shape[0]):
             o, _ = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False)
@@ -272,7 +310,7 @@ class WanBlockFn(torch.autograd.Function):
         x, e, context, *params = fctx.saved_tensors
         meta, names = fctx.meta, fctx.names
         P = dict(zip(names, params))
-        W = BF16Weights(P)
+        W = BF16Weights(P, fp8=meta.fp8)
         G = {}
         dxs, des, dcs = [], [], []
         for b in range(x.shape[0]):

@@ -140,6 +140,8 @@ def _rope_table(freqs, device):
 class WanAttentionBlock(nn.Module):
     """model.py:280-359.  forward() is one fused, activation-checkpointed HIP autograd node."""
 
+    fp8_gemm = False    # config C5's fp8 path (WanModel.set_fp8_gemm); the reference is bf16-only
+
     def __init__(self, cross_attn_type, dim, ffn_dim, num_heads, window_size=(-1, -1),
                  qk_norm=True, cross_attn_norm=False, eps=1e-6):
         super().__init__()
@@ -168,7 +170,7 @@ class WanAttentionBlock(nn.Module):
             P = {n: params[n] for n in self._names}
             meta = B.Meta(self.num_heads, [tuple(g) for g in grid_sizes.tolist()],
                           [int(s) for s in seq_lens.tolist()], _rope_table(freqs, x.device),
-                          self.i2v, self.eps)
+                          self.i2v, self.eps, fp8=self.fp8_gemm)
             ctx = context if context.dtype == torch.bfloat16 else context.to(torch.bfloat16)
             return B.block_apply(P, x.contiguous(), em.contiguous(), ctx.contiguous(), meta)
 
@@ -257,6 +259,15 @@ class WanModel(nn.Module):
         if model_type in ("i2v", "flf2v"):
             self.img_emb = MLPProj(1280, dim, flf_pos_emb=model_type == "flf2v")
         self.init_weights()
+
+    def set_fp8_gemm(self, on=True):
+        """Config C5 (`train_prfl_i2v_720`, "fp8 MFMA path"): every block's large forward
+        projections — QKV, self-attn O, cross-attn q/o, FFN in/out — run as per-row e4m3 operands
+        on the block-scaled fp8 MFMA; the backward GEMMs stay bf16 (straight-through).  Held to
+        SURVEY §8c's 5e-2 against the bf16 path, not to the reference (which is bf16-only)."""
+        for blk in self.blocks:
+            blk.fp8_gemm = bool(on)
+        return self
 
     # ---------------------------------------------------------------- checkpoint I/O --------
     @classmethod

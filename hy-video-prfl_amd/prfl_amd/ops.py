@@ -62,6 +62,45 @@ def linear_dw(dy, x, out=None, accumulate=False):
     return gemm(dy, x, out, N, K, M, False, False, EPI_F32, accumulate=accumulate)
 
 
+FP8 = torch.float8_e4m3fn   # OCP e4m3 (gfx950), not the MI300 fnuz variant
+
+
+def quant_rows_fp8(x, q=None, scale=None):
+    """Per-row e4m3 quantisation: scale[m] = amax_m / 448, q = e4m3(x * 448 / amax_m).
+    x [M, K] bf16 or fp32 (row-strided), K % 8 == 0, K <= 16384."""
+    _lib.require_gpu(x)
+    M, K = x.shape
+    if q is None:
+        q = torch.empty(M, K, dtype=FP8, device=x.device)
+    if scale is None:
+        scale = torch.empty(M, dtype=torch.float32, device=x.device)
+    assert x.dtype in (BF16, torch.float32) and q.dtype == FP8
+    call("prfl_quant_rows_fp8", ptr(x), I32(int(x.dtype == torch.float32)), I64(_ld(x)), I64(M),
+         I64(K), ptr(q), I64(_ld(q)), ptr(scale), stream_ptr())
+    return q, scale
+
+
+def linear_fp8(xq, xs, wq, ws, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None,
+               aux=None):
+    """y = (xs * xq) @ (ws * wq)^T (+bias, epilogue) on the block-scaled fp8 MFMA: xq [M,K],
+    wq [N,K] e4m3 with per-row fp32 scales xs [M], ws [N]."""
+    _lib.require_gpu(xq, wq)
+    assert xq.dtype == FP8 and wq.dtype == FP8
+    assert bias is None or (bias.dtype == BF16 and bias.is_contiguous())
+    assert gate is None or (gate.dtype == torch.float32 and gate.is_contiguous())
+    M, K = xq.shape
+    N = wq.shape[0]
+    if out is None:
+        dt = torch.float32 if epilogue == EPI_RESID else BF16
+        out = torch.empty(M, N, dtype=dt, device=xq.device)
+    call("prfl_gemm_fp8", ptr(xq), I64(_ld(xq)), ptr(xs), ptr(wq), I64(_ld(wq)), ptr(ws),
+         ptr(out), I64(_ld(out)), I64(M), I64(N), I64(K), I32(epilogue), ptr(bias), ptr(gate),
+         ptr(res), I64(_ld(res) if res is not None else 0),
+         I32(int(res is not None and res.dtype == BF16)), ptr(aux),
+         I64(_ld(aux) if aux is not None else 0), stream_ptr())
+    return out
+
+
 def cast_bf16(src, dst=None):
     """fp32 -> bf16 (round to nearest even); dst may be a contiguous slice of a larger buffer."""
     _lib.require_gpu(src)

@@ -115,6 +115,21 @@ int prfl_scale(float* x, int64_t n, const float* factor, void* stream);
 int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, void* stream);
 
+/* ---- fp8 path (config C5, train_prfl_i2v_720 "fp8 MFMA path"; SURVEY §8c tolerance 5e-2 vs
+ * the bf16 path).  The reference itself is bf16-only; these replace the same autocast
+ * nn.Linear forwards as prfl_gemm_bf16 when the fp8 path is enabled.
+ * prfl_quant_rows_fp8: per-row OCP e4m3 quantisation of x [M][K] (bf16, or fp32 if x_f32):
+ *   scale[m] = amax_m / 448, q[m][k] = e4m3(x[m][k] * 448 / amax_m)   (K % 8 == 0, K <= 16384)
+ * prfl_gemm_fp8: C = sa[m] * sb[n] * sum_k A(m,k) B(n,k) with A [M][K], B [N][K] e4m3 K-major,
+ *   block-scaled MFMA (unit block scales), epilogue 0/1/2 as prfl_gemm_bf16 (bias bf16 [N]);
+ *   K % 128 == 0, lda/ldb % 16 == 0, 16-B aligned A/B/sb. */
+int prfl_quant_rows_fp8(const void* x, int x_f32, int64_t ldx, int64_t M, int64_t K, void* q,
+                        int64_t ldq, float* scale, void* stream);
+int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const void* B, int64_t ldb,
+                  const float* sb, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                  int epilogue, const void* bias, const float* gate, const void* res, int64_t ldr,
+                  int res_bf16, void* aux, int64_t ldaux, void* stream);
+
 /* ---- FlowUniPC sampler update (bh2, order <= 2, x0-prediction) ----------------------------
  * Replaces the element-wise body of FlowUniPCMultistepScheduler.step
  * (diffusers_lite/wan/utils/fm_solvers_unipc.py:655-739: convert_model_output :321, UniC

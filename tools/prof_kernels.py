@@ -51,7 +51,24 @@ elif which == "gemmfwd":
         torch.cuda.synchronize()
         dt = (time.time() - t0) / reps
         print(f"gemm {name} {L}x{N}x{K} {dt*1e3:.2f} ms  {2*L*N*K/dt/1e12:.0f} TF/s", flush=True)
-        del x, w, y
+        # the fp8 path (C5): per-row quantisation of x + block-scaled fp8 MFMA GEMM
+        wq, ws = ops.quant_rows_fp8(w)
+        xq, xs = ops.quant_rows_fp8(x)
+        ops.linear_fp8(xq, xs, wq, ws, out=y)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for i in range(reps):
+            ops.linear_fp8(xq, xs, wq, ws, out=y)
+        torch.cuda.synchronize()
+        dt8 = (time.time() - t0) / reps
+        t0 = time.time()
+        for i in range(reps):
+            ops.quant_rows_fp8(x, xq, xs)
+        torch.cuda.synchronize()
+        dtq = (time.time() - t0) / reps
+        print(f"  fp8 {dt8*1e3:.2f} ms  {2*L*N*K/dt8/1e12:.0f} TF/s;  quant x {dtq*1e3:.2f} ms "
+              f"({L*K*3/dtq/1e9:.0f} GB/s)", flush=True)
+        del x, w, y, wq, xq
 else:
     x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(F, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
