@@ -796,6 +796,233 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------- forward, ping-pong v3 (NKT x 32-key tiles) ---
+// attn_fwd_pp2_kernel with the key tile widened to NKT * 32 keys (NKT = 3: 96 keys, a 144 KiB
+// 3-stage ring): per-tile fixed costs (two barriers, row-max exchange, rescale test, DMA issue)
+// amortised over 1.5x the MFMA work.  Same per-element arithmetic; the online-softmax rescale
+// points move to 96-key boundaries (FA numerics, not bit-identical to pp2).
+template <bool SHORT_KV, int SCHED, int NKT>
+__global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
+  constexpr bool STAMP = false;
+  constexpr int TK = NKT * 32;                 // keys per tile
+  constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
+  constexpr int SB = 2 * SV;                   // bytes of one [K | V] ring stage
+  __shared__ __attribute__((aligned(16))) char smem[3 * SB];   // ring of [K | V] tiles
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gp = w >> 2;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+
+  bf16x8 qf[8];
+  {
+    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = NEG_INF, lsum = 0.f;
+  const int nkv = (a.k_len + TK - 1) / TK;
+
+  // hoisted LDS read offsets (bytes within a [K | V] stage)
+  int koff[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) koff[ks] = off16(l32, ks * 2 + hh);   // + kt*32 rows
+  // (rows r and r + 8 of a transposed read carry different swizzles; + 16 s2 + 32 kt rows keep them)
+  int voff[4], voff8[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    voff[dt] = SV + offB(4 * (g >> 1) + qq, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
+    voff8[dt] = SV + offB(4 * (g >> 1) + qq + 8, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
+  }
+  // hoisted DMA source offsets (elements) of this lane's two K and two V 16-B chunks
+  int64_t ksrc[NKT], vsrc[NKT];
+  int drow[NKT];
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) {
+    const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+    drow[i] = row;
+    ksrc[i] = (int64_t)row * a.ldk + ((pc ^ (row & 15)) << 3);
+    vsrc[i] = (int64_t)row * a.ldv + ((pc ^ swzb) << 3);
+  }
+  const bool clamp_last = (int64_t)nkv * TK > a.Lk;
+  auto dma = [&](int t, int st) {
+    char* Ks = smem + st * SB;
+    char* Vs = Ks + SV;
+    if (clamp_last && t == nkv - 1) {
+#pragma unroll
+      for (int i = 0; i < NKT; ++i) {
+        const int piece = w * NKT + i, row = drow[i], pc = lane & 15;
+        const int key = min(t * TK + row, a.Lk - 1);
+        const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+        dma16(Kb + (int64_t)key * a.ldk + ((pc ^ (row & 15)) << 3), lds_addr(Ks + piece * 1024));
+        dma16(Vb + (int64_t)key * a.ldv + ((pc ^ swzb) << 3), lds_addr(Vs + piece * 1024));
+      }
+    } else {
+      const bf16* kt0 = Kb + (int64_t)t * TK * a.ldk;
+      const bf16* vt0 = Vb + (int64_t)t * TK * a.ldv;
+#pragma unroll
+      for (int i = 0; i < NKT; ++i) {
+        const int piece = w * NKT + i;
+        dma16(kt0 + ksrc[i], lds_addr(Ks + piece * 1024));
+        dma16(vt0 + vsrc[i], lds_addr(Vs + piece * 1024));
+      }
+    }
+  };
+  auto bar = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  dma(0, 0);
+  if (nkv > 1) dma(1, 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+  bar();
+  if (gp == 1) {
+    __builtin_amdgcn_s_setprio(1);
+    bar();
+  }
+
+  f32x16 s[NKT];
+  bf16x8 pf[NKT][2];
+  int st = 0, stp = 2;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, sx = 0, sxb = 0, sy = 0, syb = 0;
+  if (STAMP) t0 = stamp();
+  for (int t = 0; t <= nkv; ++t) {
+    // ---------------- X_t ----------------
+    if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+    if (t < nkv) {
+      const char* Ks = smem + st * SB;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], (f32x16){});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks)
+          s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
+      }
+      if (SCHED) {   // K-row reads SCHED+1 MFMAs ahead, one per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 1, 0);
+#pragma unroll
+        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
+      }
+    }
+    if (t > 0) {
+      const char* Vs = smem + stp * SB;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int ro = (kt * 32 + 16 * s2) * 256;
+            const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
+            o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
+          }
+      }
+      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
+#pragma unroll
+        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
+      }
+    }
+    if (STAMP) t1 = stamp();
+    if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (STAMP) t2 = stamp();
+    // ---------------- Y_t ----------------
+    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
+    if (t < nkv) {
+      const int kbase = t * TK;
+      if (kbase + TK > a.k_len) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+      mx = xhalf_max(mx);
+      const float mnew = fmaxf(m, mx * a.sl2);
+      if (__any(mnew > m)) {                    // rescale only when a row max grew
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        lsum *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        m = mnew;
+      }
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[kt][r] * a.sl2 - m);
+          s[kt][r] = p;
+          lsum += p;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
+                                f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
+                                f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
+                                f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+      }
+    }
+    if (STAMP) t3 = stamp();
+    if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (STAMP) {
+      const unsigned long long t4 = stamp();
+      sx += t1 - t0; sxb += t2 - t1; sy += t3 - t2; syb += t4 - t3;
+      t0 = t4;
+    }
+    stp = st;
+    st = st == 2 ? 0 : st + 1;
+  }
+  if (STAMP && a.stamps && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 16 && lane == 0) {
+    unsigned long long* o = a.stamps + (blockIdx.x * 8 + w) * 4;
+    o[0] = sx; o[1] = sxb; o[2] = sy; o[3] = syb;
+  }
+  if (gp == 0) bar();
+  lsum += __shfl_xor(lsum, 32, 64);
+  const int qr = q0 + w * 32 + l32;
+  if (qr < a.Lq) {
+    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
+    const float inv = 1.f / lsum;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * inv);
+        *(bf16x4*)(Ob + dt * 32 + 8 * rg + 4 * hh) = v;
+      }
+    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m + log2f(lsum);
+  }
+}
+
 // ============================================================================ backward ===
 // delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128)
 __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
@@ -1531,9 +1758,17 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   prfl_prof::begin(kid, s);
   static const int impl = getenv("PRFL_ATTN_FWD16") ? 16 : getenv("PRFL_ATTN_FWD32") ? 32
                           : getenv("PRFL_ATTN_PP1") ? 2 : 3;
-  static const int sched = getenv("PRFL_ATTN_SCHED") ? atoi(getenv("PRFL_ATTN_SCHED")) : 1;
+  // default: pp3 (96-key tiles) at SCHED 2; PRFL_ATTN_NKT=2 selects pp2 (64-key tiles, SCHED 1)
+  static const int nkt = getenv("PRFL_ATTN_NKT") ? atoi(getenv("PRFL_ATTN_NKT")) : 3;
+  static const int sched = getenv("PRFL_ATTN_SCHED") ? atoi(getenv("PRFL_ATTN_SCHED"))
+                                                      : (nkt == 3 ? 2 : 1);
   const dim3 g2((Lq + 255) / 256, H, B);
-  if (impl == 3 && sched == 1) {
+  if (impl == 3 && nkt == 3) {
+    if (kid != KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp3_kernel<true, 1, 3>), g2, dim3(512), 0, s, a);
+    else if (sched == 0) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 0, 3>), g2, dim3(512), 0, s, a);
+    else if (sched == 2) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 2, 3>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 1, 3>), g2, dim3(512), 0, s, a);
+  } else if (impl == 3 && sched == 1) {
     if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 1>), g2, dim3(512), 0, s, a);
     else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 1>), g2, dim3(512), 0, s, a);
   } else if (impl == 3 && sched == 3) {

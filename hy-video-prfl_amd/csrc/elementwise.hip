@@ -83,6 +83,37 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, int P, int 
   out[c] = accumulate ? out[c] + s : s;
 }
 
+// 16 column lanes (4 columns each) x 16 row lanes per workgroup: a [P][N] partial-sum matrix is
+// reduced with every workgroup streaming 64 columns of all P rows (16-B loads, 4 in flight per
+// lane), then the 16 row-lane sums are added in a fixed order (deterministic).
+__global__ __launch_bounds__(NT) void colsum_reduce4_kernel(const float* __restrict__ part, int P,
+                                                            int N, float* __restrict__ out,
+                                                            int accumulate) {
+  __shared__ f32x4 red[16][16];
+  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cx * 4;
+  f32x4 s0 = {0, 0, 0, 0}, s1 = s0, s2 = s0, s3 = s0;
+  if (c < N) {
+    int p = ry;
+    for (; p + 48 < P; p += 64) {
+      s0 += *(const f32x4*)(part + (int64_t)p * N + c);
+      s1 += *(const f32x4*)(part + (int64_t)(p + 16) * N + c);
+      s2 += *(const f32x4*)(part + (int64_t)(p + 32) * N + c);
+      s3 += *(const f32x4*)(part + (int64_t)(p + 48) * N + c);
+    }
+    for (; p < P; p += 16) s0 += *(const f32x4*)(part + (int64_t)p * N + c);
+  }
+  red[ry][cx] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ry == 0 && c < N) {
+    f32x4 t = red[0][cx];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) t += red[r][cx];
+    if (accumulate) t += *(const f32x4*)(out + c);
+    *(f32x4*)(out + c) = t;
+  }
+}
+
 __global__ void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
   __shared__ float red[NT / 64];
   float s = 0.f;
@@ -198,8 +229,12 @@ extern "C" int prfl_colsum_reduce(const float* part, int64_t P, int64_t N, float
                                   int accumulate, void* stream) {
   if (N <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((N + NT - 1) / NT), dim3(NT), 0, s, part, (int)P,
-                     (int)N, out, accumulate);
+  if (N % 4 == 0 && ((uintptr_t)part & 15) == 0 && ((uintptr_t)out & 15) == 0)
+    hipLaunchKernelGGL(colsum_reduce4_kernel, dim3((N + 63) / 64), dim3(NT), 0, s, part, (int)P,
+                       (int)N, out, accumulate);
+  else
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((N + NT - 1) / NT), dim3(NT), 0, s, part,
+                       (int)P, (int)N, out, accumulate);
   PRFL_LAUNCH_CHECK();
   return 0;
 }

@@ -17,6 +17,8 @@
 // The backward is the transpose of that linear map as torch autograd evaluates it (same
 // rounding of the gradient to bf16 where autograd casts it to a bf16 input's dtype, and the
 // same accumulation order into m_t: D1 path, then c1 path, then the corrector path).
+#include <string.h>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -152,11 +154,24 @@ __global__ __launch_bounds__(NT) void unipc_bwd_kernel(UniPCCoef k, const bf16* 
   }
 }
 
+// host-side round-to-nearest-even to bf16 (the reference casts the solved rhos to the sample
+// dtype, fm_solvers_unipc.py:612); NaN/inf pass through
+float round_bf16(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  if ((u & 0x7f800000u) != 0x7f800000u) u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+  float r;
+  memcpy(&r, &u, 4);
+  return r;
+}
+
 bool load_coef(const float* c, int corr, int pred, UniPCCoef& k) {
   if (corr < 0 || corr > 2 || pred < 1 || pred > 2 || !c) return false;
   k.sig = c[0];
   k.corr = corr;
-  k.c_r = c[1]; k.c_c1 = c[2]; k.c_rk = c[3]; k.c_rho0 = c[4]; k.c_rhoL = c[5]; k.c_aBh = c[6];
+  k.c_r = c[1]; k.c_c1 = c[2]; k.c_rk = c[3]; k.c_aBh = c[6];
+  k.c_rho0 = round_bf16(c[4]);
+  k.c_rhoL = round_bf16(c[5]);
   k.pred = pred;
   k.p_r = c[7]; k.p_c1 = c[8]; k.p_rk = c[9]; k.p_aBh = c[10];
   return true;

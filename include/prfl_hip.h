@@ -139,7 +139,7 @@ int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const void* B, in
  * hist2 (= model_outputs[-2]) / m_t are fp32, all n contiguous elements.
  * coef[11] (host) = {sigma_i, corrector: sig_t/sig_s0, alpha_t*h_phi_1, rk, rho0, rho_last,
  *                    alpha_t*B_h, predictor: sig_t/sig_s0, alpha_t*h_phi_1, rk, alpha_t*B_h}
- * with rho0/rho_last already rounded to bf16 (the reference casts the solved rhos, :612).
+ * rho0/rho_last are rounded to bf16 on entry (the reference casts the solved rhos, :612).
  * corr_order 0 = no corrector (then last_sample/hist2 may be NULL, sample_c optional).
  * Bit-identical to the reference's torch chain (fp32 ops in its order, no FMA contraction). */
 int prfl_unipc_step(const void* sample, const float* model_output, const void* last_sample,

@@ -275,3 +275,17 @@ def test_sumsq_scale(ops):
     y = x.clone()
     ops.scale_(y, f)
     assert torch.equal(y, x * 0.5)
+
+
+@pytest.mark.parametrize("P,N", [(1155, 5120), (7, 64), (33, 13824), (1, 4), (64, 6)])
+def test_colsum_reduce(ops, P, N):
+    """[P][N] partial column sums -> [N] (bias / LN-affine gradients), fresh and accumulating."""
+    g = torch.Generator(device=DEV).manual_seed(P * N)
+    part = torch.randn(P, N, generator=g, device=DEV)
+    ref = part.double().sum(0)
+    out = ops.colsum_reduce(part)
+    assert (out.double() - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+    base = torch.randn(N, generator=g, device=DEV)
+    out2 = base.clone()
+    ops.colsum_reduce(part, out=out2, accumulate=True)
+    assert (out2.double() - (ref + base.double())).abs().max().item() <= 1e-4
