@@ -11,6 +11,8 @@
 // The column reductions of the backward passes (d scale, d shift, d w, d b) are written as
 // per-workgroup partial rows and summed by colsum_reduce (elementwise.hip) — no float atomics,
 // bitwise reproducible.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -309,6 +311,80 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
   }
 }
 
+// Same arithmetic as ln_mod_fwd_kernel with the per-column coefficients — (1 + scale, shift) or
+// (w, b) — staged once per workgroup in LDS and each wave normalising RPW rows in turn: the
+// one-row-per-wave kernel re-read 8 B of coefficients from L2 for every 4 B of x.
+constexpr int RPW = 4;   // rows per wave -> 16 rows per workgroup
+__global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
+    const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ w,
+    const float* __restrict__ b, float eps, bf16* __restrict__ out, int64_t ldo,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  __shared__ f32x4 cA[WV * 64], cB[WV * 64];
+  const int nc = C / 4;
+  for (int c = threadIdx.x; c < nc; c += NT) {
+    if (w) {
+      cA[c] = ldf4(w, c * 4);
+      cB[c] = b ? ldf4(b, c * 4) : (f32x4){0, 0, 0, 0};
+    } else {
+      const f32x4 sc = ldf4(scale, c * 4);
+      cA[c] = (f32x4){1.f + sc[0], 1.f + sc[1], 1.f + sc[2], 1.f + sc[3]};
+      cB[c] = ldf4(shift, c * 4);
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RPW;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int64_t row = row0 + rr;
+    if (row >= L) return;
+    f32x4 v[WV];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        v[j] = ld4(x, row * ldx + c * 4, x_bf16);
+        s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+      }
+    }
+    const float mean = wave_sum(s) / C;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = v[j][r] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float var = wave_sum(ss) / C;
+    const float rstd = rsqrtf(var + eps);
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int c = lane + j * 64;
+      if (c < nc) {
+        const f32x4 a = cA[c], bb = cB[c];
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float xh = (v[j][r] - mean) * rstd;
+          if (!w && x_bf16) xh = bfr(xh);  // WanLayerNorm.type_as(x) for a bf16 input
+          o[r] = f2bf(mul_rn(xh, a[r]) + bb[r]);
+        }
+        *(bf16x4*)(out + row * ldo + c * 4) = o;
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
 constexpr int BWD_ROWS = 32;
 bool bad_c(int64_t C) { return C <= 0 || (C % 4) != 0 || C > 4 * MAXV * NT; }
 }  // namespace
@@ -323,9 +399,15 @@ extern "C" int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L
   if (bad_c(C) || (!w && (!scale || !shift))) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  hipLaunchKernelGGL(ln_mod_fwd_kernel, dim3((L + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, s, x,
-                     x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps, (bf16*)out, ldo, mean,
-                     rstd);
+  static const bool one_row = getenv("PRFL_LN_ONEROW") != nullptr;
+  if (one_row)
+    hipLaunchKernelGGL(ln_mod_fwd_kernel, dim3((L + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, s, x,
+                       x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps, (bf16*)out, ldo, mean,
+                       rstd);
+  else
+    hipLaunchKernelGGL(ln_mod_fwd_lds_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
+                       dim3(NT), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps,
+                       (bf16*)out, ldo, mean, rstd);
   prfl_prof::set_work((double)L * C * ((x_bf16 ? 2 : 4) + 2));
   prfl_prof::end(KID_LN, s);
   PRFL_LAUNCH_CHECK();

@@ -37,6 +37,22 @@ if which in ("attn", "attn_bwd"):
     for kname, d in ops.prof_collect().items():
         if d["count"]:
             print(f"  {kname}: {d['ms']:.2f} ms  {d['work'] / (d['ms'] * 1e-3) / 1e12:.0f} TF/s", flush=True)
+elif which == "ln":
+    # LN + AdaLN modulate forward at L tokens (fp32 residual in, bf16 out), and the affine norm3
+    x = torch.randn(L, C, device=dev, generator=g)
+    sc, sh = 0.1 * torch.randn(C, device=dev, generator=g), 0.1 * torch.randn(C, device=dev, generator=g)
+    for name, kw in (("mod", dict(scale=sc, shift=sh)), ("affine", dict(w=1 + sc, b=sh))):
+        y, m, r = ops.ln_mod_fwd(x, **kw)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for i in range(reps):
+            ops.ln_mod_fwd(x, out=y, **kw)
+        torch.cuda.synchronize()
+        dt = (time.time() - t0) / reps
+        ck = (y.double().sum().item(), y.double().abs().sum().item(), m.double().sum().item(),
+              r.double().sum().item())
+        print(f"ln_mod_fwd {name} {L}x{C}: {dt*1e3:.3f} ms  {L*C*6/dt/1e9:.0f} GB/s  checksum {ck}",
+              flush=True)
 elif which == "gemmfwd":
     # the forward projections of one block at L tokens (the rollout's hot GEMMs), bf16 epilogue
     for (N, K, name) in [(3 * C, C, "qkv"), (C, C, "o/cq/co"), (F, C, "ffn1"), (C, F, "ffn2")]:
