@@ -1465,6 +1465,112 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq8_kernel(AttnBwdArgs a) {
   }
 }
 
+// attn_bwd_dq8_kernel with NKT x 32-key K/V tiles (same per-element arithmetic and order).
+template <int NKT>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq8w_kernel(AttnBwdArgs a) {
+  constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
+    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
+  }
+  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
+  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
+  f32x16 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+  const int nkv = (a.k_len + TK - 1) / TK;
+  // K / V tile by LDS-DMA: 16 + 16 pieces of 4 rows, 2 + 2 per wave, swizzles on the source
+  auto dma = [&](int t, int st) {
+    char* Ks = smem + st * SB;
+    char* Vs = Ks + SV;
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+      const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+      const int kr = min(t * TK + row, a.Lk - 1);
+      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+      dma16(Kb + (int64_t)kr * a.ldk + ((pc ^ swzb) << 3), lds_addr(Ks + piece * 1024));
+      dma16(Vb + (int64_t)kr * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
+    }
+  };
+  dma(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
+  __syncthreads();
+  for (int t = 0; t < nkv; ++t) {
+    const int kb = t * TK;
+    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
+    if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
+    const char* Ks = smem + (t & 1) * SB;
+    const char* Vs = Ks + SV;
+    bf16x8 dsp[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+      const int row = kt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
+        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
+        dpt[r] = p * (dpt[r] - del);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
+          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  const int qo = q0 + w * 32 + l32;
+  if (qo < a.Lq) {
+    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
+        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
+      }
+  }
+}
+
 // dK, dV: 4 waves x 32 keys (K, V fragments and dK^T, dV^T accumulators resident, one wave per
 // SIMD); sweeps query tiles of 64 (two 32-query halves).  S = Q.K^T and dP = dO.V^T with the key
 // on the lane, so P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.
@@ -1821,6 +1927,7 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
   static const bool bwd16 = getenv("PRFL_ATTN_BWD16") != nullptr;
   static const bool dkdv4 = getenv("PRFL_ATTN_DKDV4") != nullptr;
   static const bool dq32old = getenv("PRFL_ATTN_DQ32") != nullptr;
+  static const bool dqw3 = getenv("PRFL_ATTN_DQ64") == nullptr;   // default: 96-key K/V tiles
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
   if (bwd16)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
@@ -1835,7 +1942,8 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
   if (bwd16)
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL(dq32old ? attn_bwd_dq32_kernel : attn_bwd_dq8_kernel, dim3((Lq + 255) / 256, H, B),
+    hipLaunchKernelGGL(dq32old ? attn_bwd_dq32_kernel
+                       : dqw3 ? attn_bwd_dq8w_kernel<3> : attn_bwd_dq8_kernel, dim3((Lq + 255) / 256, H, B),
                        dim3(512), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
