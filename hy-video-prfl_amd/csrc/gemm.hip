@@ -38,7 +38,27 @@ struct GemmArgs {
   int64_t ldr; int res_bf16;
   bf16* aux; int64_t ldaux;  // GELU: pre-activation out; RESID: y out; DGELU: pre-activation in
   int accumulate;       // EPI_F32: C += acc
+  const float* sa = nullptr;   // fp8 path: per-row dequant scales of A [M]
+  const float* sb = nullptr;   //           per-row dequant scales of B [N]
 };
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// two 16-B K-major fragments (bf16 kernel's k-steps s = 0, 1 of one 128-B row chunk pair) as one
+// 32-element e4m3 operand: lane (g = lane>>4) holds bytes [16g, 16g+16) and [64+16g, 64+16g+16)
+// of its row.  A and B use the same k permutation, so the dot product is unchanged.
+__device__ __forceinline__ i32x8 cat_fp8(bf16x8 lo, bf16x8 hi) {
+  const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
+  return (i32x8){(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2],
+                 (int)b[3]};
+}
+
+// block-scaled MFMA 16x16x128 e4m3 (2x the bf16 rate; the unscaled fp8 forms run at the bf16
+// rate): cbsz = blgp = 0 (both e4m3), opsel 0 -> byte 0 of each scale word = 127 = 2^0
+__device__ __forceinline__ f32x4 mfma_fp8(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0,
+                                                          0x7f7f7f7f);
+}
 
 // 32-B granule swizzle of MN-major rows: k bits {0,1,3} -> the 8 k-rows one ds_read_b64_tr_b16
 // lane group touches (q = k&3, g&1 = k>>3 bit) land on 8 different granules (conflict-free)
@@ -425,8 +445,12 @@ __device__ __forceinline__ void dma_half(char* lds, const bf16* __restrict__ P, 
   }
 }
 
-template <bool A_KC, bool B_KC, int EPI>
+template <bool A_KC, bool B_KC, int EPI, bool F8 = false>
 __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
+  // F8: A / B are e4m3 [rows][K8] passed as bf16 [rows][K8/2] (same bytes: the LDS images and
+  // LDS-DMA of the bf16 schedule move exactly the right bytes); each phase issues 8 block-scaled
+  // 16x16x128 MFMAs (same MFMA cycles as the 16 bf16 16x16x32 ones, 2x the FLOPs)
+  static_assert(!F8 || (A_KC && B_KC), "fp8 operands are K-major");
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A_h0|A_h1|B_h0|B_h1]
   int tm, tn;
   tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
@@ -460,6 +484,7 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
 
   // phase reads: 0: A_h0 + B_h0 | 1: B_h1 | 2: A_h1 (into the A_h0 registers) | 3: none
   bf16x8 af[4][2], bl[2][2], bh[2][2];
+  i32x8 af8[4], bl8[2], bh8[2];          // F8: the two k-steps' chunks as one e4m3 operand
   for (int t = 0; t < nk; ++t) {
     const char* st = smem + (t & 1) * 2 * TILE2;
 #pragma unroll
@@ -467,34 +492,73 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
       const int k = 4 * t + p;
       if (p == 0 || p == 2) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (F8) {
+            const char* base = st + (p == 0 ? 0 : HALF);
+            af8[i] = cat_fp8(read_frag<A_KC>(base, wr * 64 + i * 16, 0, lane),
+                             read_frag<A_KC>(base, wr * 64 + i * 16, 1, lane));
+          } else {
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            af[i][s] = read_frag<A_KC>(st + (p == 0 ? 0 : HALF), wr * 64 + i * 16, s, lane);
+            for (int s = 0; s < 2; ++s)
+              af[i][s] = read_frag<A_KC>(st + (p == 0 ? 0 : HALF), wr * 64 + i * 16, s, lane);
+          }
+        }
       }
       if (p == 0 || p == 1) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (F8) {
+            const char* base = st + (p == 0 ? 2 : 3) * HALF;
+            const i32x8 f = cat_fp8(read_frag<B_KC>(base, wc * 32 + j * 16, 0, lane),
+                                    read_frag<B_KC>(base, wc * 32 + j * 16, 1, lane));
+            if (p == 0) bl8[j] = f; else bh8[j] = f;
+          } else {
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 f = read_frag<B_KC>(st + (p == 0 ? 2 : 3) * HALF, wc * 32 + j * 16, s, lane);
-            if (p == 0) bl[j][s] = f; else bh[j][s] = f;
+            for (int s = 0; s < 2; ++s) {
+              const bf16x8 f = read_frag<B_KC>(st + (p == 0 ? 2 : 3) * HALF, wc * 32 + j * 16, s, lane);
+              if (p == 0) bl[j][s] = f; else bh[j][s] = f;
+            }
           }
+        }
       }
       if (k + 6 < nph) issue(t + 1 + ((p + 2) >> 2), (p + 2) & 3);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F8) {
+        // pin the cluster between its barriers: hipcc otherwise hoists the (register-only)
+        // scaled MFMAs across them; the empty asm statements make the operands "defined" after
+        // the lgkmcnt wait and the accumulators "used" before the vmcnt wait
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(af8[i]));
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) {
+          if (p & 1) asm volatile("" : "+v"(bh8[j]));
+          else asm volatile("" : "+v"(bl8[j]));
+        }
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
             const int ai = (p >> 1) * 4 + i, bj = (p & 1) * 2 + j;
-            acc[ai][bj] = mfma16((p & 1) ? bh[j][s] : bl[j][s], af[i][s], acc[ai][bj]);
+            acc[ai][bj] = mfma_fp8((p & 1) ? bh8[j] : bl8[j], af8[i], acc[ai][bj]);
           }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[(p >> 1) * 4 + i][(p & 1) * 2 + j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const int ai = (p >> 1) * 4 + i, bj = (p & 1) * 2 + j;
+              acc[ai][bj] = mfma16((p & 1) ? bh[j][s] : bl[j][s], af[i][s], acc[ai][bj]);
+            }
+      }
       __builtin_amdgcn_s_setprio(0);
       const int out = nph - 4 - k;          // half-tiles allowed in flight after this phase
       if (out >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -510,11 +574,18 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
     if (m >= g.M) continue;
+    const float s_m = F8 ? g.sa[m] : 1.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
       if (n >= g.N) continue;
-      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
+      f32x4 v = acc[i][j];
+      if constexpr (F8) {
+        const f32x4 s_n = *(const f32x4*)(g.sb + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] * (s_m * s_n[r]);
+      }
+      epilogue_tile<A_KC, B_KC, EPI>(g, v, m, n);
     }
   }
 }
@@ -610,7 +681,6 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
 // the bf16 kernel's; each lane's fragment is 32 consecutive k (two 16-B chunks).
 namespace {
 constexpr int BK8 = 128;
-typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 struct ScaleArgs {
   const float* sa;   // [M]
@@ -638,11 +708,6 @@ __device__ __forceinline__ i32x8 read_frag8(const char* lds, int base, int lane)
                  (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
-__device__ __forceinline__ f32x4 mfma_fp8(i32x8 a, i32x8 b, f32x4 c) {
-  // cbsz = blgp = 0: both operands e4m3; opsel 0 picks byte 0 of the scale words: 127 = 2^0
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0,
-                                                          0x7f7f7f7f);
-}
 
 template <int EPI>
 __global__ __launch_bounds__(NT2, 1) void gemm256_fp8_kernel(GemmArgs g, ScaleArgs sc) {
@@ -802,8 +867,23 @@ extern "C" int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const 
   ScaleArgs sc{sa, sb};
   hipStream_t s = (hipStream_t)stream;
   const int nt = (int)(((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2));
+  static const bool simple = getenv("PRFL_FP8_SIMPLE") != nullptr;
   prfl_prof::begin(KID_GEMM, s);
-  if (epilogue == EPI_BF16)
+  if (!simple) {
+    // the staggered 4-phase bf16 schedule over the same bytes: K8 e4m3 = K8/2 "bf16" columns
+    GemmArgs g2 = g;
+    g2.lda = lda / 2;
+    g2.ldb = ldb / 2;
+    g2.K = (int)(K / 2);
+    g2.sa = sa;
+    g2.sb = sb;
+    if (epilogue == EPI_BF16)
+      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_BF16, true>), dim3(nt), dim3(NT2), 0, s, g2);
+    else if (epilogue == EPI_GELU)
+      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_GELU, true>), dim3(nt), dim3(NT2), 0, s, g2);
+    else
+      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_RESID, true>), dim3(nt), dim3(NT2), 0, s, g2);
+  } else if (epilogue == EPI_BF16)
     hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_BF16>, dim3(nt), dim3(NT2), 0, s, g, sc);
   else if (epilogue == EPI_GELU)
     hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_GELU>, dim3(nt), dim3(NT2), 0, s, g, sc);
