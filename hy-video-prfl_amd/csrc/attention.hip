@@ -890,8 +890,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
   bar();
   if (gp == 1) {
+    if (a.stagger == 0) __builtin_amdgcn_s_setprio(1);   // PRFL_ATTN_PRIO: 0 default, 1 none,
+    bar();                                               // 2 the leading half instead
+  } else if (a.stagger == 2) {
     __builtin_amdgcn_s_setprio(1);
-    bar();
   }
 
   f32x16 s[NKT];
@@ -1859,6 +1861,7 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
              scale * 1.4426950408889634f, getenv("PRFL_ATTN_STAGGER") ? 1 : 0, nullptr};
+  static const int prio = getenv("PRFL_ATTN_PRIO") ? atoi(getenv("PRFL_ATTN_PRIO")) : 0;
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
@@ -1870,6 +1873,7 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
                                                       : (nkt == 3 ? 2 : 1);
   const dim3 g2((Lq + 255) / 256, H, B);
   if (impl == 3 && nkt == 3) {
+    a.stagger = prio;   // pp3 reads it as the priority mode
     if (kid != KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp3_kernel<true, 1, 3>), g2, dim3(512), 0, s, a);
     else if (sched == 0) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 0, 3>), g2, dim3(512), 0, s, a);
     else if (sched == 2) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 2, 3>), g2, dim3(512), 0, s, a);
