@@ -131,6 +131,11 @@ def pmc_traffic(L):
     return None, None
 
 
+def big_fits(args):
+    """The attention stash is sized for the 14B generator at <= 720p x 81f on a 288 GB GPU."""
+    return args.workload.startswith("prfl")
+
+
 def heartbeat(period=60.0):
     """A progress line on stderr every `period` s (a 720p iteration runs for minutes)."""
     import threading
@@ -170,6 +175,14 @@ def main():
     if args.fp8:
         gen.set_fp8_gemm(True)
         lrm.set_fp8_gemm(True)
+    # keep the self-attention outputs of the first blocks of every grad-enabled model forward
+    # for the backward (bit-identical to recomputing them): 12 GB ~ 15 blocks at 720p on one GPU
+    # (peak 257 -> 272 GB reserved), 6 GB with RCCL's buffers beside it (N > 1); off for I2V,
+    # whose 16.4 B parameters leave no headroom (peak 281.5 GB reserved)
+    from prfl_amd import block as _blk
+    stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB",
+                                    "0" if i2v or not big_fits(args) else ("12" if world == 1 else "6")))
+    _blk.set_attn_stash_budget(int(stash_gb * 1e9))
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
     text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=dev)).to(torch.bfloat16)

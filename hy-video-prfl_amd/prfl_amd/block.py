@@ -34,6 +34,23 @@ def param_names(i2v):
     return SA_NAMES + CA_NAMES + (I2V_NAMES if i2v else []) + FFN_NAMES
 
 
+# Attention-output stash (memory-for-time trade on top of the reference's per-block checkpoint):
+# a block whose forward runs with grad may keep its self-attention output and LSE (L*C*2 + H*L*4
+# bytes per sample) so the backward's recompute skips the L x L attention forward — the kernels
+# are deterministic, so the recomputed and the kept tensors are bit-identical.  The budget is per
+# model forward (WanModel.forward resets it); 0 (the default) keeps the pure checkpoint.
+_STASH = {"budget": 0, "left": 0}
+
+
+def set_attn_stash_budget(nbytes):
+    _STASH["budget"] = int(nbytes)
+    _STASH["left"] = int(nbytes)
+
+
+def reset_attn_stash():
+    _STASH["left"] = _STASH["budget"]
+
+
 class Meta:
     """Non-tensor block arguments."""
 
@@ -114,8 +131,10 @@ def _split_ctx(ctx, i2v):
     return ctx[n_img:], ctx[:n_img]
 
 
-def block_forward_one(P, W, x, e, ctx, meta, b, save):
-    """One sample: x [L, C] (fp32, or bf16 for block 0), e [6, C] fp32, ctx [Lc, C] bf16."""
+def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False):
+    """One sample: x [L, C] (fp32, or bf16 for block 0), e [6, C] fp32, ctx [Lc, C] bf16.
+    attn: a kept (ao, lse) of this sample's self-attention (skips the attention forward);
+    keep_attn: return it in S["attn"] even when not saving for the backward."""
     g = P.__getitem__
     L, C = x.shape
     nh, eps = meta.num_heads, meta.eps
@@ -127,7 +146,9 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save):
     grid = meta.grid[b]
     qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid)
     kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
-    ao, lse = ops.attn_fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
+    ao, lse = attn if attn is not None else ops.attn_fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
+    if keep_attn:
+        S["attn"] = (ao, lse)
     y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
     x1 = lin(W, "o", ao, epilogue=EPI_RESID, gate=e[2], res=x, aux=y1)
     if save:
@@ -296,11 +317,20 @@ class WanBlockFn(torch.autograd.Function):
     def forward(fctx, x, e, context, meta, names, *params):
         P = dict(zip(names, params))
         W = BF16Weights(P, fp8=meta.fp8, need_bf16=False)
-        outs = []
+        L, C = x.shape[1], x.shape[2]
+        need = x.shape[0] * (L * C * 2 + meta.num_heads * L * 4)
+        keep = any(fctx.needs_input_grad) and _STASH["left"] >= need
+        if keep:
+            _STASH["left"] -= need
+        outs, kept = [], []
         for b in range(x.shape[0]):
-            o, _ = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False)
+            o, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False,
+                                     keep_attn=keep)
             outs.append(o)
+            if keep:
+                kept.append(S["attn"])
         del W
+        fctx.attn = kept if keep else None
         fctx.meta, fctx.names = meta, names
         fctx.save_for_backward(x, e, context, *params)
         return outs[0].unsqueeze(0) if len(outs) == 1 else torch.stack(outs)
@@ -313,8 +343,10 @@ class WanBlockFn(torch.autograd.Function):
         W = BF16Weights(P, fp8=meta.fp8)
         G = {}
         dxs, des, dcs = [], [], []
+        kept, fctx.attn = fctx.attn, None
         for b in range(x.shape[0]):
-            _, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=True)
+            _, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=True,
+                                     attn=kept[b] if kept else None)
             d = dout[b].to(torch.float32).contiguous().clone()
             dx, de, dc = block_backward_one(P, W, x[b], e[b], context[b], meta, b, S, d, G,
                                             want_w=any(fctx.needs_input_grad[5:]))

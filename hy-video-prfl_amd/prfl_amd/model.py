@@ -348,6 +348,7 @@ class WanModel(nn.Module):
                                                                  clip_fea, y)
         feats = []
         h = xb
+        B.reset_attn_stash()          # per-forward budget of kept attention outputs (block.py)
         for index, block in enumerate(self.blocks):
             h = block(h, e0, seq_lens, grid_sizes, self.freqs, ctx, None)
             if output_features and index + 1 in selected_layers:

@@ -105,3 +105,31 @@ def test_real_width_block_vs_reference(golden, tag):
             assert abs(gn / float(v) - 1) < 3e-2, (n, gn, float(v))
             assert abs(gp - float(g["gproj/" + n])) < 5e-2 * float(v), (n, gp, float(g["gproj/" + n]))
     assert abs(dmod.double().norm().item() / float(g["gnorm/modulation"]) - 1) < 3e-2
+
+
+def test_attention_stash_is_bit_identical():
+    """Keeping the self-attention output/LSE for the backward (block.set_attn_stash_budget)
+    gives bit-identical outputs and gradients to the plain checkpoint recompute."""
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    dim, ffn, nh = 256, 512, 2
+    P = seeded_params(block_shapes("blocks.0.", dim, ffn, False), prefix="stash.")
+    g = torch.Generator().manual_seed(3)
+    L, grid = 105, (3, 5, 7)
+    x = torch.randn(1, L, dim, generator=g)
+    e = torch.randn(1, 6, dim, generator=g) * 0.1 + P["blocks.0.modulation"]
+    ctx = torch.randn(1, 512, dim, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, dim, generator=g)
+    res = []
+    try:
+        for budget in (0, 1 << 30):
+            B.set_attn_stash_budget(budget)
+            Pd = {n: P["blocks.0." + n].to(DEV).requires_grad_(True) for n in B.param_names(False)}
+            xd = x.to(DEV).requires_grad_(True)
+            meta = B.Meta(nh, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), False)
+            out = B.block_apply(Pd, xd, e.to(DEV), ctx.to(DEV), meta)
+            (out * up.to(DEV)).sum().backward()
+            res.append([out.detach(), xd.grad] + [p.grad for p in Pd.values()])
+    finally:
+        B.set_attn_stash_budget(0)
+    assert all(torch.equal(a, b) for a, b in zip(*res))
