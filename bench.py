@@ -176,12 +176,14 @@ def main():
         gen.set_fp8_gemm(True)
         lrm.set_fp8_gemm(True)
     # keep the self-attention outputs of the first blocks of every grad-enabled model forward
-    # for the backward (bit-identical to recomputing them): 12 GB ~ 15 blocks at 720p on one GPU
-    # (peak 257 -> 272 GB reserved), 6 GB with RCCL's buffers beside it (N > 1); off for I2V,
-    # whose 16.4 B parameters leave no headroom (peak 281.5 GB reserved)
+    # for the backward (bit-identical to recomputing them).  32 GB keeps all 40 blocks at 720p
+    # (0.76 GB each), so no grad-enabled L x L attention forward is recomputed: peak 247 GB
+    # allocated of the 309 GB (288 GiB) card at N = 1, 143.98 s/iter vs 147.8 s at 12 GB and
+    # 153.2 s without (profiles/r01_bench_prfl720_notes.txt); RCCL's own buffers (N > 1) are a few
+    # GB beside that.
     from prfl_amd import block as _blk
     stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB",
-                                    "0" if i2v or not big_fits(args) else ("12" if world == 1 else "6")))
+                                    "0" if i2v or not big_fits(args) else "32"))
     _blk.set_attn_stash_budget(int(stash_gb * 1e9))
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
