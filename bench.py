@@ -176,14 +176,17 @@ def main():
         gen.set_fp8_gemm(True)
         lrm.set_fp8_gemm(True)
     # keep the self-attention outputs of the first blocks of every grad-enabled model forward
-    # for the backward (bit-identical to recomputing them).  32 GB keeps all 40 blocks at 720p
-    # (0.76 GB each), so no grad-enabled L x L attention forward is recomputed: peak 247 GB
-    # allocated of the 309 GB (288 GiB) card at N = 1, 143.98 s/iter vs 147.8 s at 12 GB and
-    # 153.2 s without (profiles/r01_bench_prfl720_notes.txt); RCCL's own buffers (N > 1) are a few
-    # GB beside that.
+    # for the backward (bit-identical to recomputing them).  T2V: 32 GB keeps all 40 blocks at
+    # 720p (0.76 GB each), so no grad-enabled L x L attention forward is recomputed: peak 247 GB
+    # allocated / 290 GB reserved of the 309 GB (288 GiB) card at N = 1, 143.98 s/iter vs 147.8 s
+    # at 12 GB and 153.2 s without (profiles/r01_bench_prfl720_notes.txt); 20 GB (peak 281 GB
+    # reserved) when RCCL's buffers sit beside it (N > 1).  I2V (16.4 B parameters): 16 GB at
+    # N = 1 (peak 254 allocated / 302 reserved; 32 GB runs out of memory), none at N > 1.
     from prfl_amd import block as _blk
-    stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB",
-                                    "0" if i2v or not big_fits(args) else "32"))
+    default_gb = "0"
+    if big_fits(args):
+        default_gb = ("16" if world == 1 else "0") if i2v else ("32" if world == 1 else "20")
+    stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB", default_gb))
     _blk.set_attn_stash_budget(int(stash_gb * 1e9))
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank
     latents = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=dev).to(torch.bfloat16)
