@@ -2,6 +2,8 @@
   strided : q, k, v column slices of one [L, 3C] tensor (ld = 3C), raw N(0,1)
   sep     : q, k contiguous [L, C] copies (ld = C), v strided (the block's layout), raw N(0,1)
   rms     : as sep, q/k through the block's RMSNorm + 3-D RoPE kernel (the block's data)
+  corr    : as rms, but every token = 0.8 * a shared per-channel vector + 0.6 * noise (tokens
+            correlated the way hidden states become after a few blocks; same per-element scale)
 usage: PRFL_PROF_L=73920 python tools/attn_layout_probe.py [reps]"""
 import os
 import sys
@@ -31,7 +33,12 @@ tab = ops.rope_table(torch.cat([_freqs(44), _freqs(42), _freqs(42)], dim=1), dev
 w = torch.ones(C, device=dev)
 qr, _ = ops.rms_rope_fwd(q, w, 1e-6, tab, grid)
 kr, _ = ops.rms_rope_fwd(k, w, 1e-6, tab, grid)
-cases = {"strided": (q, k, v), "sep": (q.contiguous(), k.contiguous(), v), "rms": (qr, kr, v)}
+common = torch.randn(1, 3 * C, device=dev, generator=g)
+qkvc = (0.8 * common + 0.6 * torch.randn(L, 3 * C, device=dev, generator=g)).to(torch.bfloat16)
+qc, _ = ops.rms_rope_fwd(qkvc[:, :C], w, 1e-6, tab, grid)
+kc, _ = ops.rms_rope_fwd(qkvc[:, C:2 * C], w, 1e-6, tab, grid)
+cases = {"strided": (q, k, v), "sep": (q.contiguous(), k.contiguous(), v), "rms": (qr, kr, v),
+         "corr": (qc, kc, qkvc[:, 2 * C:])}
 fl = 4 * L * L * C
 for name, (a, b, c) in cases.items():
     o, lse = ops.attn_fwd(a, b, c, NH)
