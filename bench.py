@@ -29,8 +29,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# fewer, growable segments: the 720p step's live set is ~220 GB of mixed-size tensors
-os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
+# (no allocator options: this PyTorch-ROCm build ignores expandable_segments - "not supported on
+# this platform" - so the plain caching allocator serves the 720p step; its fragmentation is the
+# gap between peak_alloc_gb_rank0 and peak_hbm_gb)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hy-video-prfl_amd")]
 
 import torch  # noqa: E402

@@ -4,7 +4,10 @@
   rms     : as sep, q/k through the block's RMSNorm + 3-D RoPE kernel (the block's data)
   corr    : as rms, but every token = 0.8 * a shared per-channel vector + 0.6 * noise (tokens
             correlated the way hidden states become after a few blocks; same per-element scale)
-usage: PRFL_PROF_L=73920 python tools/attn_layout_probe.py [reps]"""
+  sharp   : as rms with q scaled by 8 (peaked softmax: most P entries underflow to 0)
+usage: PRFL_PROF_L=73920 [PRFL_PROF_WARM_S=seconds] python tools/attn_layout_probe.py [reps]
+PRFL_PROF_FILL_GB allocates (and touches) that much HBM before the operands, as the bench's
+resident model state does.  PRFL_PROF_WARM_S keeps the GPU busy on the first case for that long before anything is timed."""
 import os
 import sys
 import time
@@ -18,6 +21,8 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 L, C, NH = int(os.environ.get("PRFL_PROF_L", 73920)), 5120, 40
 grid = {73920: (21, 44, 80), 32760: (21, 30, 52)}.get(L, (1, 1, L))
 dev = "cuda"
+_fill = [torch.ones(int(2e9), dtype=torch.uint8, device=dev)
+         for _ in range(int(float(os.environ.get("PRFL_PROF_FILL_GB", "0")) / 2))]
 g = torch.Generator(device=dev).manual_seed(0)
 qkv = torch.randn(L, 3 * C, device=dev, generator=g).to(torch.bfloat16)
 q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
@@ -38,8 +43,15 @@ qkvc = (0.8 * common + 0.6 * torch.randn(L, 3 * C, device=dev, generator=g)).to(
 qc, _ = ops.rms_rope_fwd(qkvc[:, :C], w, 1e-6, tab, grid)
 kc, _ = ops.rms_rope_fwd(qkvc[:, C:2 * C], w, 1e-6, tab, grid)
 cases = {"strided": (q, k, v), "sep": (q.contiguous(), k.contiguous(), v), "rms": (qr, kr, v),
-         "corr": (qc, kc, qkvc[:, 2 * C:])}
+         "corr": (qc, kc, qkvc[:, 2 * C:]), "sharp": ((qr.float() * 8).to(torch.bfloat16), kr, v)}
 fl = 4 * L * L * C
+warm_s = float(os.environ.get("PRFL_PROF_WARM_S", "0"))
+if warm_s > 0:
+    o, _ = ops.attn_fwd(q, k, v, NH)
+    t0 = time.time()
+    while time.time() - t0 < warm_s:
+        ops.attn_fwd(q, k, v, NH, out=o)
+        torch.cuda.synchronize()
 for name, (a, b, c) in cases.items():
     o, lse = ops.attn_fwd(a, b, c, NH)
     torch.cuda.synchronize()
