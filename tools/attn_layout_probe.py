@@ -7,7 +7,7 @@
   sharp   : as rms with q scaled by 8 (peaked softmax: most P entries underflow to 0)
 usage: PRFL_PROF_L=73920 [PRFL_PROF_WARM_S=seconds] python tools/attn_layout_probe.py [reps]
 PRFL_PROF_FILL_GB allocates (and touches) that much HBM before the operands, as the bench's
-resident model state does.  PRFL_PROF_WARM_S keeps the GPU busy on the first case for that long before anything is timed."""
+resident model state does.  PRFL_PROF_GAP_S idles the GPU that long before each timed launch.  PRFL_PROF_WARM_S keeps the GPU busy on the first case for that long before anything is timed."""
 import os
 import sys
 import time
@@ -44,8 +44,14 @@ qc, _ = ops.rms_rope_fwd(qkvc[:, :C], w, 1e-6, tab, grid)
 kc, _ = ops.rms_rope_fwd(qkvc[:, C:2 * C], w, 1e-6, tab, grid)
 cases = {"strided": (q, k, v), "sep": (q.contiguous(), k.contiguous(), v), "rms": (qr, kr, v),
          "corr": (qc, kc, qkvc[:, 2 * C:]), "sharp": ((qr.float() * 8).to(torch.bfloat16), kr, v)}
+# sink: corr with key 0 scaled x4, so every row's max sits in the first key tile (no rescale
+# after it) and every other probability underflows towards 0
+kcs = kc.clone()
+kcs[0] = (kcs[0].float() * 4).to(torch.bfloat16)
+cases["sink"] = (qc, kcs, qkvc[:, 2 * C:])
 fl = 4 * L * L * C
 warm_s = float(os.environ.get("PRFL_PROF_WARM_S", "0"))
+gap_s = float(os.environ.get("PRFL_PROF_GAP_S", "0"))
 if warm_s > 0:
     o, _ = ops.attn_fwd(q, k, v, NH)
     t0 = time.time()
@@ -57,6 +63,8 @@ for name, (a, b, c) in cases.items():
     torch.cuda.synchronize()
     ts = []
     for i in range(reps):
+        if gap_s > 0:
+            time.sleep(gap_s)
         t0 = time.time()
         ops.attn_fwd(a, b, c, NH, out=o)
         torch.cuda.synchronize()
