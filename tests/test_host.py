@@ -99,3 +99,17 @@ def test_flowmatch_product_vs_reference(golden):
     t, s = fm.get_train_timestep_and_sigma(weighting_scheme="uniform", batch_size=1, n_dim=5)
     assert np.array_equal(t.numpy(), g["fm_sample_t"])
     assert np.array_equal(s.numpy(), g["fm_sample_sigma"])
+
+
+def test_bench_stash_only_where_moments_leave_hbm():
+    """bench.py keeps attention outputs only on the 720p workloads (AdamW moments on the host);
+    at 480p the moments stay in HBM and a stash beside them runs out of memory."""
+    import argparse
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("prfl_bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    fits = {w: bench.big_fits(argparse.Namespace(workload=w))
+            for w in ("prfl_t2v_720", "prfl_i2v_720", "prfl_t2v_480", "pavrm_t2v_480")}
+    assert fits == {"prfl_t2v_720": True, "prfl_i2v_720": True, "prfl_t2v_480": False,
+                    "pavrm_t2v_480": False}
