@@ -20,13 +20,24 @@ large forward projections as per-row e4m3 on the block-scaled fp8 MFMA, backward
 Multi-GPU: pure data parallel (weak scaling, one sample per rank), RCCL all-reduce of the
 generator gradients overlapped with the backward (prfl_amd/dist.py).  `value` = PRFL sample-
 iterations completed by all ranks per second.
+
+Wall-clock budget (`--budget-s`, default 540 s from interpreter start, inside the driver's 600 s):
+a 720p iteration takes minutes, so `--warmup W` runs min(W, 1) warm-up iterations at
+mid_timestep = 1 (every kernel, both optimizer updates and the memory high-water mark of the
+full iteration, minus 18 no-grad rollout forwards), then up to `--steps K` full iterations are
+timed — as many as the budget holds, at least one; `steps` reports how many ran.  Every timed
+iteration is an optimizer-step iteration ((step + 1) % 5 == 0: SFT and reward AdamW updates
+inside it, the slowest of the five), so the window always ends on an optimizer step.
 """
-import argparse
-import json
-import math
-import os
-import sys
 import time
+
+T_START = time.time()   # the driver's clock starts with the interpreter; the budget counts from here
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import math  # noqa: E402
+import os  # noqa: E402
+import sys  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # (no allocator options: this PyTorch-ROCm build ignores expandable_segments - "not supported on
@@ -139,6 +150,14 @@ def big_fits(args):
     return args.workload.startswith("prfl") and args.workload.endswith("720")
 
 
+def draw_mid(rank, world, dev):
+    """mid_timestep = randint(0, 38) drawn on rank 0 and broadcast (train_prfl.py:640-651)."""
+    t = torch.randint(0, 39, (1,), device=dev) if rank == 0 else torch.zeros(1, dtype=torch.long, device=dev)
+    if world > 1:
+        dist.broadcast(t, 0)
+    return int(t.item())
+
+
 def heartbeat(period=60.0):
     """A progress line on stderr every `period` s (a 720p iteration runs for minutes)."""
     import threading
@@ -162,6 +181,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp8", action="store_true",
                     help="config C5's fp8 path: e4m3 forward projections on the block-scaled MFMA")
+    ap.add_argument("--budget-s", type=float, default=540.0,
+                    help="wall-clock budget from interpreter start (warm-up + timed + CPU baseline)")
+    ap.add_argument("--warmup-mid", type=int, default=1,
+                    help="mid_timestep of the warm-up iterations (full iterations: use --mid)")
+    ap.add_argument("--random-mid", action="store_true",
+                    help="draw mid_timestep = randint(0, 38) per iteration on rank 0 and broadcast "
+                         "it, as train_prfl.py:640-651 does (default: fixed --mid)")
     args = ap.parse_args()
     world, rank, local = setup()
     dev = torch.device("cuda", local)
@@ -213,12 +239,19 @@ def main():
                          optimizer_shard=big and world > 1,
                          optimizer_overlap=os.environ.get("PRFL_OPT_OVERLAP", "1") == "1")
 
-        def one(step):
+        mids = []
+
+        def one(step, mid=None):
+            if mid is None:
+                mid = draw_mid(rank, world, dev) if args.random_mid else args.mid
+                mids.append(mid)
             a = tr.sft_step(step, latents, text, L, image_embeds=clip, cond=cond, generator=g)
             b = tr.reward_step(step, latents, text, L, image_embeds=clip, cond=cond,
-                               mid_timestep=args.mid, generator=g)
+                               mid_timestep=mid, generator=g)
             return a, b
-        flops_it = iteration_flops(L, args.mid, i2v)
+
+        def flops_of(mid):
+            return iteration_flops(L, mid, i2v)
     else:
         del gen
         for blk in lrm.blocks:
@@ -226,18 +259,29 @@ def main():
         tr = PAVRMTrainer(lrm, qa, mlp)
         label = torch.ones(1, device=dev)
 
-        def one(step):
-            return tr.step(latents, text, L, label, generator=g), None
-        flops_it = 3 * 8 * block_fwd_flops(L)
+        mids = []
 
-    # step indices: the timed window ends on an optimizer-step iteration ((step+1) % 5 == 0)
-    first = max(0, (5 - (args.warmup + args.steps) % 5) % 5)
-    for s in range(first, first + args.warmup):
+        def one(step, mid=None):
+            return tr.step(latents, text, L, label, generator=g), None
+
+        def flops_of(mid):
+            return 3 * 8 * block_fwd_flops(L)
+
+    prfl = args.workload.startswith("prfl")
+    # warm-up: min(W, 1) iterations at a short rollout (see the module docstring); step index 4
+    # is an optimizer-step iteration, so both AdamW updates are warmed as well
+    n_warm = min(args.warmup, 1)
+    t_warm = None
+    for _ in range(n_warm):
         t_w = time.time()
-        one(s)
+        one(4, mid=args.warmup_mid if prfl else None)
         torch.cuda.synchronize()
+        t_warm = time.time() - t_w
         if rank == 0:
-            print(f"[bench] warmup iteration {s}: {time.time() - t_w:.1f} s", file=sys.stderr, flush=True)
+            print(f"[bench] warm-up iteration (mid_timestep {args.warmup_mid}): {t_warm:.1f} s",
+                  file=sys.stderr, flush=True)
+    # the CPU baseline runs after the timed window: keep room for it in the budget
+    cpu_reserve = 0.0 if (args.no_cpu_baseline or rank != 0 or world > 1) else 45.0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -247,12 +291,25 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.time()
-    for s in range(first + args.warmup, first + args.warmup + args.steps):
-        last = one(s)
+    steps, durs = 0, []
+    for i in range(args.steps):
+        last = one(9 + 5 * i)            # every timed iteration ends on an optimizer step
+        torch.cuda.synchronize()
+        steps += 1
+        t_it = time.time() - t0 - sum(durs)
+        durs.append(t_it)
+        est = max(sum(durs) / steps, t_it)     # the next iteration must fit the budget
+        left = args.budget_s - (time.time() - T_START) - cpu_reserve
+        go = torch.tensor([1.0 if left > 1.1 * est else 0.0], device=dev)
+        if world > 1:                      # every rank runs the same number of iterations
+            dist.all_reduce(go, op=dist.ReduceOp.MIN)
+        if go.item() == 0.0:
+            break
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.time() - t0
+    flops_it = sum(flops_of(m) for m in mids) / len(mids) if mids else flops_of(args.mid)
     ops.prof_enable(False)
     prof = ops.prof_collect()
     peak_alloc = torch.cuda.max_memory_allocated() / 1e9
@@ -271,22 +328,26 @@ def main():
     d = prof[dom]
     achieved = d["work"] / (d["ms"] * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(L)
-    value = world * args.steps / dt
+    value = world * steps / dt
     res = {
         "metric": "PRFL train steps/sec (whole node) + peak HBM GB, 14B DiT",
         "value": round(value, 6), "unit": "PRFL iterations/s (all ranks)",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+        "n_gpus": world, "steps": steps, "warmup": n_warm,
+        "steps_requested": args.steps, "warmup_requested": args.warmup,
+        "budget_s": args.budget_s, "wall_s_at_report": None,
+        "ms_per_step": round(dt / steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp8-e4m3 fwd GEMMs / bf16" if args.fp8 else "bf16", "data": "synthetic latents/text, random-init 14B weights",
-        "config": {"workload": ("train_%s: SFT + reward step, mid_timestep=%d" % (args.workload, args.mid)
-                                if args.workload.startswith("prfl") else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
+        "config": {"workload": (("train_%s: SFT + reward step, mid_timestep=%s" %
+                                 (args.workload, ("randint(0, 38) per iteration: %s" % mids) if args.random_mid
+                                  else args.mid))
+                                if prfl else "train_pavrm_t2v_480: 8-block trunk + head, BCE"),
                    "model": ("Wan2.1-I2V-14B (40 blocks, C=5120, image cross-attn)" if i2v
                              else "Wan2.1-T2V-14B (40 blocks, C=5120)"), "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
         "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),
         "algorithmic_tflop_per_step": round(flops_it / 1e12, 1),
-        "achieved_tflops_per_gpu": round(flops_it * args.steps / dt / 1e12, 1),
+        "achieved_tflops_per_gpu": round(flops_it * steps / dt / 1e12, 1),
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 1),
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
@@ -299,7 +360,7 @@ def main():
                         "rate": round(v["work"] / (v["ms"] * 1e-3) / (1e9 if k in ("ln", "rms", "eltwise", "adamw") else 1e12), 1)}
                     for k, v in prof.items() if v["count"]},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         cdt, cfl, thr = cpu_baseline()
         cpu_rate = cfl / cdt
         res["cpu_baseline"] = {"value": flops_it and cpu_rate / flops_it, "unit": "PRFL iterations/s",
@@ -307,6 +368,7 @@ def main():
                                "sample": f"oracle fp32 14B block fwd+bwd at L=4096 on host: {cdt:.1f} s "
                                          f"({cpu_rate/1e12:.2f} TFLOP/s), extrapolated by FLOPs to one "
                                          f"iteration ({flops_it/1e15:.1f} PFLOP)"}
+    res["wall_s_at_report"] = round(time.time() - T_START, 1)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -5,16 +5,17 @@
 // [B, L, H*128] (row stride ld), so q/k/v come straight out of the fused QKV GEMM with no
 // permute.  Softmax statistics are kept in the log2 domain: LSE2 = max + log2(sum).
 //
-// Forward: one workgroup = 4 waves x 32 query rows; K/V tiles of 64 keys are register-staged
-// into a double-buffered LDS ring.  S^T = K.Q^T is computed with the key on the MFMA row so that
-// every query row lives on one lane column: the softmax statistics are per-lane scalars and the
-// S^T accumulator, packed to bf16, is directly the B operand of O^T = V^T.P^T (the 16x16x32
-// k-slot order is permuted consistently on both operands; V^T fragments come from
-// ds_read_b64_tr_b16 on the row-major V tile).
+// Lane geometry shared by every kernel here: MFMA 32x32x16 bf16 with the key (forward, dQ) or
+// the query (dK/dV) on the MFMA row, so the other index lives on one lane column: softmax
+// statistics are per-lane scalars and an f32 accumulator packed to bf16 is directly the B
+// operand of the next product (the 32x32x16 k-slot order is permuted consistently on both
+// operands); transposed operands come from ds_read_b64_tr_b16 on row-major LDS images.
 //
-// Backward (FA2 recomputation, no atomics): delta = rowsum(dO*O); a dK/dV kernel owns 128 keys
-// per workgroup (32 per wave, accumulators resident) and sweeps all query tiles; a dQ kernel owns
-// 128 queries and sweeps all key tiles.  Both reuse the same lane mappings as the forward.
+// Kernels (one of each; no alternative schedules):
+//   attn_fwd_kernel       forward, 8 waves x 32 queries, 96-key K/V tiles, ping-pong wave groups
+//   attn_delta_kernel     D = rowsum(dO * O) (FA2)
+//   attn_bwd_dkdv_kernel  dK, dV: 8 waves x 32 keys, Q/dO tiles streamed, no atomics
+//   attn_bwd_dq_kernel    dQ: 8 waves x 32 queries, 96-key K/V tiles streamed
 #include <stdlib.h>
 
 #include "common.h"
@@ -31,8 +32,6 @@ struct AttnArgs {
   float* LSE;            // [B][H][Lq], log2 domain
   int Lq, Lk, H, k_len;
   float sl2;             // softmax_scale * log2(e)
-  int stagger;           // attn_fwd32: waves 4-7 run one phase behind waves 0-3
-  unsigned long long* stamps;   // diagnostic build only (prfl_attn_fwd_stamped), else null
 };
 
 struct AttnBwdArgs {
@@ -84,726 +83,33 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
                   f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
 }
 
-// ============================================================================ forward ====
-// SHORT_KV: separate instantiation for the 512/257-key cross-attention so profiles separate it
-// from the self-attention (same code today).
-template <bool SHORT_KV>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int qr = min(q0 + w * 32 + sub * 16 + l16, a.Lq - 1);
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds) qf[sub][ds] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ds * 32 + g * 8);
-  }
-  f32x4 o[2][8];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m[2] = {NEG_INF, NEG_INF}, l[2] = {0.f, 0.f};
-
-  const int nkv = (a.k_len + 63) / 64;
-  u32x4 rk[4], rv[4];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      const int key = min(t * 64 + row, a.Lk - 1);
-      rk[i] = *(const u32x4*)(Kb + (int64_t)key * a.ldk + ch * 8);
-      rv[i] = *(const u32x4*)(Vb + (int64_t)key * a.ldv + ch * 8);
-    }
-  };
-  auto sstore = [&](int st) {
-    char* Ks = smem + st * 32768;
-    char* Vs = Ks + 16384;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      *(u32x4*)(Ks + off16(row, ch)) = rk[i];
-      *(u32x4*)(Vs + offT(row, ch << 4)) = rv[i];
-    }
-  };
-  gload(0);
-  sstore(0);
-  __syncthreads();
-
-  for (int t = 0; t < nkv; ++t) {
-    const char* Ks = smem + (t & 1) * 32768;
-    const char* Vs = Ks + 16384;
-    if (t + 1 < nkv) gload(t + 1);
-    f32x4 s[2][4];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[sub][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds)
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const bf16x8 kf = row_frag<0>(Ks, kt * 16, ds, lane);
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) s[sub][kt] = mfma16(kf, qf[sub][ds], s[sub][kt]);
-      }
-    const int kbase = t * 64;
-    if (kbase + 64 > a.k_len) {
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kbase + kt * 16 + 4 * g + r >= a.k_len) {
-            s[0][kt][r] = NEG_INF;
-            s[1][kt][r] = NEG_INF;
-          }
-    }
-    bf16x8 pf[2][2];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      float mx = NEG_INF;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[sub][kt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[sub], mx * a.sl2);
-      const float alpha = exp2f(m[sub] - mnew);
-      float rs = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[sub][kt][r] * a.sl2 - mnew);
-          s[sub][kt][r] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l[sub] = l[sub] * alpha + rs;
-      m[sub] = mnew;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[sub][dt] *= alpha;
-      pf[sub][0] = pack8(s[sub][0], s[sub][1]);
-      pf[sub][1] = pack8(s[sub][2], s[sub][3]);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 vf = tr_frag<0>(Vs, ks * 32, dt * 16, lane);
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) o[sub][dt] = mfma16(vf, pf[sub][ks], o[sub][dt]);
-      }
-    if (t + 1 < nkv) sstore((t + 1) & 1);
-    __syncthreads();
-  }
-
-  bf16* Ob = a.O + b * a.bo + h * HD;
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int qr = q0 + w * 32 + sub * 16 + l16;
-    if (qr >= a.Lq) continue;
-    const float inv = 1.f / l[sub];
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      bf16x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[sub][dt][r] * inv);
-      *(bf16x4*)(Ob + (int64_t)qr * a.ldo + dt * 16 + 4 * g) = v;
-    }
-    if (g == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m[sub] + log2f(l[sub]);
-  }
-}
-
-// ===================================================================== forward (32x32) ====
-// 8 waves x 32 queries = 256 queries per workgroup; K/V tiles of 64 keys register-staged into a
-// 2-deep LDS ring shared by all 8 waves.  MFMA 32x32x16 (8 of its 32 issue cycles hold the SIMD's
-// vector issue, vs 8 of 16 for 16x16x32), so the softmax VALU hides under the matrix pipe.
-//   S^T[key][q] = K . Q^T  : A = K rows (ds_read_b128), B = Q^T fragments kept in registers
-//   lane (q = l&31, h = l>>5) holds keys (r&3) + 8(r>>2) + 4h of a 32-key tile in acc r
-//   P packed to bf16 straight from the accumulator (k order 16s + 8(j>>2) + 4h + (j&3)) is the
-//   B operand of O^T[d][q] += V^T . P^T, with V^T fragments read by ds_read_b64_tr_b16 in the
-//   same permuted key order.  Row max is exchanged between the two lane halves once per tile;
-//   row sums stay per-half until the end; O is rescaled only when some row max grew (exact).
-template <bool SHORT_KV>
-__global__ __launch_bounds__(512, 1) void attn_fwd32_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * 32768];
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l32 = lane & 31, hh = lane >> 5;
-  // Waves 4-7 share SIMDs with waves 0-3 and run one phase behind them: they apply tile t-1's
-  // P.V after tile t's S, so one partner's softmax VALU overlaps the other's MFMA work instead
-  // of both partners reaching it together between the same barriers.  Per-wave arithmetic and
-  // its order are unchanged (bit-identical output).  Needs a 3-stage K/V ring.
-  const bool late = a.stagger && w >= 4;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-
-  bf16x8 qf[8];
-  {
-    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-  }
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = NEG_INF, lsum = 0.f;
-
-  const int nkv = (a.k_len + 63) / 64;
-  u32x4 rk[2], rv[2];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
-      const int key = min(t * 64 + row, a.Lk - 1);
-      rk[i] = *(const u32x4*)(Kb + (int64_t)key * a.ldk + ch * 8);
-      rv[i] = *(const u32x4*)(Vb + (int64_t)key * a.ldv + ch * 8);
-    }
-  };
-  auto sstore = [&](int st) {
-    char* Ks = smem + st * 32768;
-    char* Vs = Ks + 16384;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
-      *(u32x4*)(Ks + off16(row, ch)) = rk[i];
-      *(u32x4*)(Vs + offB(row, ch << 4)) = rv[i];
-    }
-  };
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  bf16x8 pf[2][2];
-  // O^T[d][q] += V^T P^T ; V^T fragment: lane group g reads keys base + 4*(g>>1) + {0..3},
-  // base + 8 + 4*(g>>1) + {0..3}, columns d0 = dt*32 + 16*(g&1)
-  auto pv = [&](const char* Vs) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const int rb = ra + 8;
-          const bf16x8 vf = cat8(lds_read_tr(Vs + offB(ra, byte)), lds_read_tr(Vs + offB(rb, byte)));
-          o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
-        }
-    }
-  };
-  gload(0);
-  sstore(0);
-  __syncthreads();
-
-  int st = 0, st_prev = 0;
-  for (int t = 0; t < nkv; ++t) {
-    const char* Ks = smem + st * 32768;
-    if (t + 1 < nkv) gload(t + 1);
-    if (late && t > 0) pv(smem + st_prev * 32768 + 16384);
-    f32x16 s[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
-      const int row = kt * 32 + l32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + off16(row, ks * 2 + hh));
-        s[kt] = mfma32(kf, qf[ks], s[kt]);
-      }
-    }
-    const int kbase = t * 64;
-    if (kbase + 64 > a.k_len) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
-    }
-    float mx = NEG_INF;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx * a.sl2);
-    if (__any(mnew > m)) {                      // rescale only when a row max grew
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-      lsum *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-      m = mnew;
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(s[kt][r] * a.sl2 - m);
-        s[kt][r] = p;
-        lsum += p;
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
-                              f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
-                              f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
-                              f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
-    }
-    if (!late) pv(Ks + 16384);
-    st_prev = st;
-    st = st == 2 ? 0 : st + 1;
-    if (t + 1 < nkv) sstore(st);
-    __syncthreads();
-  }
-  if (late) pv(smem + st_prev * 32768 + 16384);
-  lsum += __shfl_xor(lsum, 32, 64);
-  const int qr = q0 + w * 32 + l32;
-  if (qr < a.Lq) {
-    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
-    const float inv = 1.f / lsum;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * inv);
-        *(bf16x4*)(Ob + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m + log2f(lsum);
-  }
-}
-
-// ----------------------------------------------------- forward, ping-pong wave groups ---
-// attn_fwd32's lane geometry (8 waves x 32 queries, MFMA 32x32x16, P fed from the accumulator)
-// re-scheduled so the two waves sharing a SIMD alternate roles (MI355X guide §Two waves per
-// SIMD, item 9): every tile is two barrier-delimited phases,
-//   X_t: S(t) = K(t).Q^T and O += V(t-1)^T P(t-1)   (32 MFMAs)
-//   Y_t: row max, conditional O/l rescale, P(t) = exp2(S*sl2 - m), row sums   (VALU)
-// and waves 4-7 run one barrier behind waves 0-3, so on each SIMD one wave's X overlaps its
-// partner's Y.  K/V tiles arrive by LDS-DMA into a 3-stage ring: tile T is issued in global
-// phase 2T-2 (waves 0-3 in X_{T-1}, waves 4-7 in Y_{T-2}) into the stage tile T-3 left at the
-// end of phase 2T-3, and retired by each issuing wave's vmcnt(0) before the barrier that ends
-// phase 2T-1.  Same per-element arithmetic and order as attn_fwd32_kernel.
-template <bool SHORT_KV>
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * 32768];   // ring of [K | V] tiles
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gp = w >> 2;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-
-  bf16x8 qf[8];
-  {
-    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-  }
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = NEG_INF, lsum = 0.f;
-  const int nkv = (a.k_len + 63) / 64;
-
-  // one tile = 32 pieces of 1 KiB (4 key rows each): wave w moves K pieces 2w, 2w+1 and the
-  // same V pieces; the LDS images' 16-B chunk swizzles go on each lane's SOURCE address
-  auto dma = [&](int t, int st) {
-    char* Ks = smem + st * 32768;
-    char* Vs = Ks + 16384;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = w * 2 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-      const int key = min(t * 64 + row, a.Lk - 1);
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16(Kb + (int64_t)key * a.ldk + ((pc ^ (row & 15)) << 3), lds_addr(Ks + piece * 1024));
-      dma16(Vb + (int64_t)key * a.ldv + ((pc ^ swzb) << 3), lds_addr(Vs + piece * 1024));
-    }
-  };
-  auto bar = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  dma(0, 0);
-  if (nkv > 1) dma(1, 1);
-  // a real s_waitcnt (not inline asm) so the compiler's scoreboard sees the Q fragments landed
-  // and does not re-wait vmcnt(0) for them inside the loop (it also covers tiles 0/1)
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
-  bar();
-  if (gp == 1) bar();
-
-  f32x16 s[2];
-  bf16x8 pf[2][2];
-  int st = 0, stp = 2;                     // stage of tile t, of tile t-1
-  for (int t = 0; t <= nkv; ++t) {
-    // ---------------- X_t ----------------
-    if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-    if (t < nkv) {
-      const char* Ks = smem + st * 32768;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
-        const int row = kt * 32 + l32;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-          s[kt] = mfma32(*(const bf16x8*)(Ks + off16(row, ks * 2 + hh)), qf[ks], s[kt]);
-      }
-    }
-    if (t > 0) {
-      const char* Vs = smem + stp * 32768 + 16384;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-            const bf16x8 vf = cat8(lds_read_tr(Vs + offB(ra, byte)), lds_read_tr(Vs + offB(ra + 8, byte)));
-            o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
-          }
-      }
-    }
-    if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    // ---------------- Y_t ----------------
-    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
-    if (t < nkv) {
-      const int kbase = t * 64;
-      if (kbase + 64 > a.k_len) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
-      }
-      float mx = NEG_INF;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx * a.sl2);
-      if (__any(mnew > m)) {                    // rescale only when a row max grew
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        lsum *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-        m = mnew;
-      }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[kt][r] * a.sl2 - m);
-          s[kt][r] = p;
-          lsum += p;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
-                                f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
-                                f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
-                                f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
-      }
-    }
-    if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    stp = st;
-    st = st == 2 ? 0 : st + 1;
-  }
-  if (gp == 0) bar();
-  lsum += __shfl_xor(lsum, 32, 64);
-  const int qr = q0 + w * 32 + l32;
-  if (qr < a.Lq) {
-    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
-    const float inv = 1.f / lsum;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * inv);
-        *(bf16x4*)(Ob + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m + log2f(lsum);
-  }
-}
-
-// ----------------------------------------------- forward, ping-pong v2 (address-hoisted) ---
-// attn_fwd_pp_kernel with the per-tile overheads taken out of both phases (same arithmetic, same
-// order, bit-identical output):
-//  * every LDS address is a per-lane constant hoisted out of the loop (8 K-row offsets, 4 V^T
-//    offsets: the image swizzles make them lane-dependent) plus a wave-uniform stage base and
-//    immediate offsets, instead of ~50 v_add/v_or per tile;
-//  * LDS-DMA sources are per-lane constants plus a wave-uniform tile stride (the key clamp is
-//    only needed on the last tile);
-//  * the row-max exchange between the two lane halves is one v_permlane32_swap instead of a
-//    ds_bpermute round trip on the softmax critical path;
-//  * waves 4-7 (the younger, lagging half) run at s_setprio 1 (MI355X guide, two waves per SIMD,
-//    item 4).
-// diagnostic cycle stamp (MI355X guide, in-kernel stamps): one asm statement with its lgkmcnt(0)
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-template <bool SHORT_KV, int SCHED, bool STAMP = false>
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp2_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * 32768];   // ring of [K | V] tiles
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gp = w >> 2;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-
-  bf16x8 qf[8];
-  {
-    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-  }
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = NEG_INF, lsum = 0.f;
-  const int nkv = (a.k_len + 63) / 64;
-
-  // hoisted LDS read offsets (bytes within a [K | V] stage)
-  int koff[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) koff[ks] = off16(l32, ks * 2 + hh);   // + kt*32 rows
-  // (rows r and r + 8 of a transposed read carry different swizzles; + 16 s2 + 32 kt rows keep them)
-  int voff[4], voff8[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    voff[dt] = 16384 + offB(4 * (g >> 1) + qq, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
-    voff8[dt] = 16384 + offB(4 * (g >> 1) + qq + 8, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
-  }
-  // hoisted DMA source offsets (elements) of this lane's two K and two V 16-B chunks
-  int64_t ksrc[2], vsrc[2];
-  int drow[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int piece = w * 2 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-    drow[i] = row;
-    ksrc[i] = (int64_t)row * a.ldk + ((pc ^ (row & 15)) << 3);
-    vsrc[i] = (int64_t)row * a.ldv + ((pc ^ swzb) << 3);
-  }
-  const bool clamp_last = (int64_t)nkv * 64 > a.Lk;
-  auto dma = [&](int t, int st) {
-    char* Ks = smem + st * 32768;
-    char* Vs = Ks + 16384;
-    if (clamp_last && t == nkv - 1) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int piece = w * 2 + i, row = drow[i], pc = lane & 15;
-        const int key = min(t * 64 + row, a.Lk - 1);
-        const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-        dma16(Kb + (int64_t)key * a.ldk + ((pc ^ (row & 15)) << 3), lds_addr(Ks + piece * 1024));
-        dma16(Vb + (int64_t)key * a.ldv + ((pc ^ swzb) << 3), lds_addr(Vs + piece * 1024));
-      }
-    } else {
-      const bf16* kt0 = Kb + (int64_t)t * 64 * a.ldk;
-      const bf16* vt0 = Vb + (int64_t)t * 64 * a.ldv;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int piece = w * 2 + i;
-        dma16(kt0 + ksrc[i], lds_addr(Ks + piece * 1024));
-        dma16(vt0 + vsrc[i], lds_addr(Vs + piece * 1024));
-      }
-    }
-  };
-  auto bar = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  dma(0, 0);
-  if (nkv > 1) dma(1, 1);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
-  bar();
-  if (gp == 1) {
-    __builtin_amdgcn_s_setprio(1);
-    bar();
-  }
-
-  f32x16 s[2];
-  bf16x8 pf[2][2];
-  int st = 0, stp = 2;
-  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, sx = 0, sxb = 0, sy = 0, syb = 0;
-  if (STAMP) t0 = stamp();
-  for (int t = 0; t <= nkv; ++t) {
-    // ---------------- X_t ----------------
-    if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-    if (t < nkv) {
-      const char* Ks = smem + st * 32768;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], (f32x16){});
-#pragma unroll
-        for (int ks = 1; ks < 8; ++ks)
-          s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
-      }
-      if (SCHED) {   // K-row reads SCHED+1 MFMAs ahead, one per MFMA gap
-        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 1, 0);
-#pragma unroll
-        for (int i = 0; i < 15 - SCHED; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
-      }
-    }
-    if (t > 0) {
-      const char* Vs = smem + stp * 32768;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int ro = (kt * 32 + 16 * s2) * 256;
-            const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
-            o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
-          }
-      }
-      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
-#pragma unroll
-        for (int i = 0; i < 15 - SCHED; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
-      }
-    }
-    if (STAMP) t1 = stamp();
-    if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (STAMP) t2 = stamp();
-    // ---------------- Y_t ----------------
-    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
-    if (t < nkv) {
-      const int kbase = t * 64;
-      if (kbase + 64 > a.k_len) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
-      }
-      float mx = NEG_INF;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-      mx = xhalf_max(mx);
-      const float mnew = fmaxf(m, mx * a.sl2);
-      if (__any(mnew > m)) {                    // rescale only when a row max grew
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        lsum *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-        m = mnew;
-      }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[kt][r] * a.sl2 - m);
-          s[kt][r] = p;
-          lsum += p;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
-                                f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
-                                f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
-                                f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
-      }
-    }
-    if (STAMP) t3 = stamp();
-    if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (STAMP) {
-      const unsigned long long t4 = stamp();
-      sx += t1 - t0; sxb += t2 - t1; sy += t3 - t2; syb += t4 - t3;
-      t0 = t4;
-    }
-    stp = st;
-    st = st == 2 ? 0 : st + 1;
-  }
-  if (STAMP && a.stamps && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 16 && lane == 0) {
-    unsigned long long* o = a.stamps + (blockIdx.x * 8 + w) * 4;
-    o[0] = sx; o[1] = sxb; o[2] = sy; o[3] = syb;
-  }
-  if (gp == 0) bar();
-  lsum += __shfl_xor(lsum, 32, 64);
-  const int qr = q0 + w * 32 + l32;
-  if (qr < a.Lq) {
-    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
-    const float inv = 1.f / lsum;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * inv);
-        *(bf16x4*)(Ob + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = m + log2f(lsum);
-  }
-}
-
-// ---------------------------------------- forward, ping-pong v3 (NKT x 32-key tiles) ---
-// attn_fwd_pp2_kernel with the key tile widened to NKT * 32 keys (NKT = 3: 96 keys, a 144 KiB
-// 3-stage ring): per-tile fixed costs (two barriers, row-max exchange, rescale test, DMA issue)
-// amortised over 1.5x the MFMA work.  Same per-element arithmetic; the online-softmax rescale
-// points move to 96-key boundaries (FA numerics, not bit-identical to pp2).
+// ============================================================================ forward ====
+// 8 waves x 32 queries = 256 queries per workgroup; K/V tiles of TK = 96 keys (NKT = 3 x 32)
+// arrive by LDS-DMA into a 3-stage ring (144 KiB).  Per tile:
+//   S^T[key][q] = K . Q^T  : A = K rows (ds_read_b128), B = Q^T fragments kept in registers;
+//     lane (q = l&31, h = l>>5) holds keys (r&3) + 8(r>>2) + 4h of each 32-key sub-tile
+//   P packed to bf16 straight from the accumulator is the B operand of O^T[d][q] += V^T . P^T,
+//     V^T fragments read by ds_read_b64_tr_b16 in the same permuted key order
+// The two waves sharing a SIMD alternate roles (MI355X guide §Two waves per SIMD, item 9):
+// every tile is two barrier-delimited phases
+//   X_t: S(t) = K(t).Q^T and O += V(t-1)^T P(t-1)   (48 MFMAs)
+//   Y_t: row max (one v_permlane32_swap between the lane halves), O / l rescale only when some
+//        row max grew (exact), P(t) = exp2(S*sl2 - m), row sums (VALU)
+// and waves 4-7 run one barrier behind waves 0-3 at s_setprio 1 (the younger half; guide item
+// 4), so on each SIMD one wave's X overlaps its partner's Y.  Tile T is issued by waves 0-3 in
+// X_{T-1} / by waves 4-7 in Y_{T-2} into the stage tile T-3 left, and retired by each issuing
+// wave's vmcnt(0) before the barrier that ends that phase.  LDS addresses and DMA sources are
+// per-lane constants hoisted out of the loop (the key clamp is only needed on the last tile).
+// SCHED > 0 interleaves the LDS reads SCHED+1 MFMAs ahead of their use (sched_group_barrier).
+// SHORT_KV: separate instantiation for the 512/257-key cross-attention (SCHED 1) so profiles
+// separate it from the self-attention (SCHED 2).
 template <bool SHORT_KV, int SCHED, int NKT>
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
-  constexpr bool STAMP = false;
+__global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
   constexpr int SB = 2 * SV;                   // bytes of one [K | V] ring stage
@@ -889,18 +195,14 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
   if (nkv > 1) dma(1, 1);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
   bar();
-  if (gp == 1) {
-    if (a.stagger == 0) __builtin_amdgcn_s_setprio(1);   // PRFL_ATTN_PRIO: 0 default, 1 none,
-    bar();                                               // 2 the leading half instead
-  } else if (a.stagger == 2) {
+  if (gp == 1) {          // the lagging (younger) half: one barrier behind, static priority 1
     __builtin_amdgcn_s_setprio(1);
+    bar();
   }
 
   f32x16 s[NKT];
   bf16x8 pf[NKT][2];
   int st = 0, stp = 2;
-  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, sx = 0, sxb = 0, sy = 0, syb = 0;
-  if (STAMP) t0 = stamp();
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
@@ -946,10 +248,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
-    if (STAMP) t1 = stamp();
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (STAMP) t2 = stamp();
     // ---------------- Y_t ----------------
     if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
     if (t < nkv) {
@@ -991,20 +291,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
                                 f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
       }
     }
-    if (STAMP) t3 = stamp();
     if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (STAMP) {
-      const unsigned long long t4 = stamp();
-      sx += t1 - t0; sxb += t2 - t1; sy += t3 - t2; syb += t4 - t3;
-      t0 = t4;
-    }
     stp = st;
     st = st == 2 ? 0 : st + 1;
-  }
-  if (STAMP && a.stamps && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 16 && lane == 0) {
-    unsigned long long* o = a.stamps + (blockIdx.x * 8 + w) * 4;
-    o[0] = sx; o[1] = sxb; o[2] = sy; o[3] = syb;
   }
   if (gp == 0) bar();
   lsum += __shfl_xor(lsum, 32, 64);
@@ -1025,6 +315,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp3_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ backward ===
 // ============================================================================ backward ===
 // delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128)
 __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
@@ -1049,667 +340,15 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int
   if (row < nrows && part == 0) delta[(b * H + h) * Lq + q] = acc;
 }
 
-// dK, dV: workgroup owns 128 keys (wave: 32 = 2 sub-tiles of 16), sweeps query tiles of 32.
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 8192];  // Q tile | dO tile
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
-  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
-
-  bf16x8 kf[2][4], vf[2][4];
-  bool kvalid[2];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int key = k0 + w * 32 + sub * 16 + l16;
-    kvalid[sub] = key < a.k_len;
-    const int kr = min(key, a.Lk - 1);
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
-      kf[sub][ds] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ds * 32 + g * 8);
-      vf[sub][ds] = *(const bf16x8*)(Vb + (int64_t)kr * a.ldv + ds * 32 + g * 8);
-    }
-  }
-  f32x4 dk[2][8], dv[2][8];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      dk[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dv[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  char* Qs = smem;
-  char* Ds = smem + 8192;
-  const int nq = (a.Lq + 31) / 32;
-  for (int t = 0; t < nq; ++t) {
-    const int qb = t * 32;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      const int qr = min(qb + row, a.Lq - 1);
-      *(u32x4*)(Qs + offB(row, ch << 4)) = *(const u32x4*)(Qb + (int64_t)qr * a.ldq + ch * 8);
-      *(u32x4*)(Ds + offB(row, ch << 4)) = *(const u32x4*)(dOb + (int64_t)qr * a.lddo + ch * 8);
-    }
-    // per-row statistics for rows q = qb + qt*16 + 4g + r
-    f32x4 lse4[2], del4[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qr = qb + qt * 16 + 4 * g + r;
-        lse4[qt][r] = qr < a.Lq ? lseb[qr] : __builtin_huge_valf();
-        del4[qt][r] = qr < a.Lq ? delb[qr] : 0.f;
-      }
-    __syncthreads();
-    bf16x8 pp[2], dsp[2];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x4 s[2], dp[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        s[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        dp[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ds = 0; ds < 4; ++ds) {
-          s[qt] = mfma16(row_frag<1>(Qs, qt * 16, ds, lane), kf[sub][ds], s[qt]);
-          dp[qt] = mfma16(row_frag<1>(Ds, qt * 16, ds, lane), vf[sub][ds], dp[qt]);
-        }
-        // s: D[q][key] with key = lane column
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = kvalid[sub] ? exp2f(s[qt][r] * a.sl2 - lse4[qt][r]) : 0.f;
-          s[qt][r] = p;
-          dp[qt][r] = p * (dp[qt][r] - del4[qt][r]);
-        }
-      }
-      pp[sub] = pack8(s[0], s[1]);
-      dsp[sub] = pack8(dp[0], dp[1]);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const bf16x8 dot = tr_frag<1>(Ds, 0, dt * 16, lane);
-      const bf16x8 qt_ = tr_frag<1>(Qs, 0, dt * 16, lane);
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        dv[sub][dt] = mfma16(dot, pp[sub], dv[sub][dt]);
-        dk[sub][dt] = mfma16(qt_, dsp[sub], dk[sub][dt]);
-      }
-    }
-    __syncthreads();
-  }
-  bf16* dKb = a.dK + b * a.bdk + h * HD;
-  bf16* dVb = a.dV + b * a.bdv + h * HD;
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int key = k0 + w * 32 + sub * 16 + l16;
-    if (key >= a.Lk) continue;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      bf16x4 vk, vv;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        vk[r] = f2bf(dk[sub][dt][r] * a.scale);
-        vv[r] = f2bf(dv[sub][dt][r]);
-      }
-      *(bf16x4*)(dKb + (int64_t)key * a.lddk + dt * 16 + 4 * g) = vk;
-      *(bf16x4*)(dVb + (int64_t)key * a.lddv + dt * 16 + 4 * g) = vv;
-    }
-  }
-}
-
-// dQ: workgroup owns 128 queries (wave: 32), sweeps key tiles of 64.
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[32768];  // K tile (image B) | V tile
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
-  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
-
-  bf16x8 qf[2][4], df[2][4];
-  float lse[2], del[2];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int qr = min(q0 + w * 32 + sub * 16 + l16, a.Lq - 1);
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
-      qf[sub][ds] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ds * 32 + g * 8);
-      df[sub][ds] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ds * 32 + g * 8);
-    }
-    lse[sub] = lseb[qr];
-    del[sub] = delb[qr];
-  }
-  f32x4 dq[2][8];
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) dq[sub][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  char* Ks = smem;
-  char* Vs = smem + 16384;
-  const int nkv = (a.k_len + 63) / 64;
-  for (int t = 0; t < nkv; ++t) {
-    const int kb = t * 64;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      const int kr = min(kb + row, a.Lk - 1);
-      *(u32x4*)(Ks + offB(row, ch << 4)) = *(const u32x4*)(Kb + (int64_t)kr * a.ldk + ch * 8);
-      *(u32x4*)(Vs + off16(row, ch)) = *(const u32x4*)(Vb + (int64_t)kr * a.ldv + ch * 8);
-    }
-    __syncthreads();
-    bf16x8 dsp[2][2];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x4 s[4], dp[4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        dp[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ds = 0; ds < 4; ++ds) {
-          s[kt] = mfma16(row_frag<1>(Ks, kt * 16, ds, lane), qf[sub][ds], s[kt]);
-          dp[kt] = mfma16(row_frag<0>(Vs, kt * 16, ds, lane), df[sub][ds], dp[kt]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb + kt * 16 + 4 * g + r;
-          const float p = key < a.k_len ? exp2f(s[kt][r] * a.sl2 - lse[sub]) : 0.f;
-          dp[kt][r] = p * (dp[kt][r] - del[sub]);
-        }
-      }
-      dsp[sub][0] = pack8(dp[0], dp[1]);
-      dsp[sub][1] = pack8(dp[2], dp[3]);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kt_ = tr_frag<1>(Ks, ks * 32, dt * 16, lane);
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) dq[sub][dt] = mfma16(kt_, dsp[sub][ks], dq[sub][dt]);
-      }
-    __syncthreads();
-  }
-  bf16* dQb = a.dQ + b * a.bdq + h * HD;
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    const int qr = q0 + w * 32 + sub * 16 + l16;
-    if (qr >= a.Lq) continue;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      bf16x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[sub][dt][r] * a.scale);
-      *(bf16x4*)(dQb + (int64_t)qr * a.lddq + dt * 16 + 4 * g) = v;
-    }
-  }
-}
-
-// ================================================================== backward (32x32) ======
-// Same lane geometry as attn_fwd32: MFMA 32x32x16, accumulators consumed in place as the next
-// product's B operand, transposed operands from ds_read_b64_tr_b16.
-//
-// dQ: 8 waves x 32 queries; per 64-key tile S^T = K.Q^T, dP^T = V.dO^T (query on the lane, so
-// LSE and D are per-lane scalars), dS^T = P^T (dP^T - D) packed to bf16, dQ^T += K^T dS^T.
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq32_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[32768];  // K tile (image B) | V tile
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-  bf16x8 qf[8], df[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
-  }
-  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
-  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
-  f32x16 dq[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-  char* Ks = smem;
-  char* Vs = smem + 16384;
-  const int nkv = (a.k_len + 63) / 64;
-  u32x4 rk[2], rv[2];
-  auto fetch = [&](int kb) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
-      const int kr = min(kb + row, a.Lk - 1);
-      rk[i] = *(const u32x4*)(Kb + (int64_t)kr * a.ldk + ch * 8);
-      rv[i] = *(const u32x4*)(Vb + (int64_t)kr * a.ldv + ch * 8);
-    }
-  };
-  fetch(0);
-  for (int t = 0; t < nkv; ++t) {
-    const int kb = t * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 512 * i, row = c >> 4, ch = c & 15;
-      *(u32x4*)(Ks + offB(row, ch << 4)) = rk[i];
-      *(u32x4*)(Vs + off16(row, ch)) = rv[i];
-    }
-    __syncthreads();
-    if (t + 1 < nkv) fetch(kb + 64);
-    bf16x8 dsp[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f32x16 st, dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
-      const int row = kt * 32 + l32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
-        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
-        dpt[r] = p * (dpt[r] - del);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
-          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
-        }
-    }
-    __syncthreads();
-  }
-  const int qo = q0 + w * 32 + l32;
-  if (qo < a.Lq) {
-    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
-        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-  }
-}
-
-// dQ, 8 waves: attn_bwd_dq32_kernel with the K / V tiles arriving by LDS-DMA into a 2-stage
-// ring (tile t+1 issued at the top of tile t, retired by vmcnt(0) + the one barrier per tile)
-// instead of register staging + ds_write + two barriers.  Same arithmetic, same order.
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq8_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];  // 2 stages of [K (image B) | V]
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-  bf16x8 qf[8], df[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
-  }
-  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
-  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
-  f32x16 dq[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-  const int nkv = (a.k_len + 63) / 64;
-  // K / V tile by LDS-DMA: 16 + 16 pieces of 4 rows, 2 + 2 per wave, swizzles on the source
-  auto dma = [&](int t, int st) {
-    char* Ks = smem + st * 32768;
-    char* Vs = Ks + 16384;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = w * 2 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-      const int kr = min(t * 64 + row, a.Lk - 1);
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16(Kb + (int64_t)kr * a.ldk + ((pc ^ swzb) << 3), lds_addr(Ks + piece * 1024));
-      dma16(Vb + (int64_t)kr * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
-    }
-  };
-  dma(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
-  __syncthreads();
-  for (int t = 0; t < nkv; ++t) {
-    const int kb = t * 64;
-    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
-    if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
-    const char* Ks = smem + (t & 1) * 32768;
-    const char* Vs = Ks + 16384;
-    bf16x8 dsp[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f32x16 st, dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
-      const int row = kt * 32 + l32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
-        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
-        dpt[r] = p * (dpt[r] - del);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
-          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  const int qo = q0 + w * 32 + l32;
-  if (qo < a.Lq) {
-    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
-        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-  }
-}
-
-// attn_bwd_dq8_kernel with NKT x 32-key K/V tiles (same per-element arithmetic and order).
-template <int NKT>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq8w_kernel(AttnBwdArgs a) {
-  constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
-  bf16x8 qf[8], df[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
-  }
-  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
-  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
-  f32x16 dq[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-  const int nkv = (a.k_len + TK - 1) / TK;
-  // K / V tile by LDS-DMA: 16 + 16 pieces of 4 rows, 2 + 2 per wave, swizzles on the source
-  auto dma = [&](int t, int st) {
-    char* Ks = smem + st * SB;
-    char* Vs = Ks + SV;
-#pragma unroll
-    for (int i = 0; i < NKT; ++i) {
-      const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-      const int kr = min(t * TK + row, a.Lk - 1);
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16(Kb + (int64_t)kr * a.ldk + ((pc ^ swzb) << 3), lds_addr(Ks + piece * 1024));
-      dma16(Vb + (int64_t)kr * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
-    }
-  };
-  dma(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
-  __syncthreads();
-  for (int t = 0; t < nkv; ++t) {
-    const int kb = t * TK;
-    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
-    if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
-    const char* Ks = smem + (t & 1) * SB;
-    const char* Vs = Ks + SV;
-    bf16x8 dsp[NKT][2];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      f32x16 st, dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
-      const int row = kt * 32 + l32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
-        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
-        dpt[r] = p * (dpt[r] - del);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
-          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  const int qo = q0 + w * 32 + l32;
-  if (qo < a.Lq) {
-    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
-        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
-      }
-  }
-}
-
-// dK, dV: 4 waves x 32 keys (K, V fragments and dK^T, dV^T accumulators resident, one wave per
-// SIMD); sweeps query tiles of 64 (two 32-query halves).  S = Q.K^T and dP = dO.V^T with the key
-// on the lane, so P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv32_kernel(AttnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[32768 + 512];  // Q | dO (image B) | LSE, D
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
-  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
-  const int key = k0 + w * 32 + l32;
-  const bool kvalid = key < a.k_len;
-  const int kr = min(key, a.Lk - 1);
-  bf16x8 kf[8], vf[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    kf[ks] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ks * 16 + hh * 8);
-    vf[ks] = *(const bf16x8*)(Vb + (int64_t)kr * a.ldv + ks * 16 + hh * 8);
-  }
-  f32x16 dk[4], dv[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-  char* Qs = smem;
-  char* Ds = smem + 16384;
-  float* Ls = (float*)(smem + 32768);   // [64] LSE (+inf past Lq), then [64] D
-  const int nq = (a.Lq + 63) / 64;
-  u32x4 rq[4], rd[4];
-  float rl = 0.f;
-  auto fetch = [&](int qb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      const int q = min(qb + row, a.Lq - 1);
-      rq[i] = *(const u32x4*)(Qb + (int64_t)q * a.ldq + ch * 8);
-      rd[i] = *(const u32x4*)(dOb + (int64_t)q * a.lddo + ch * 8);
-    }
-    if (tid < 128) {
-      const int q = qb + (tid & 63);
-      rl = tid < 64 ? (q < a.Lq ? lseb[q] : __builtin_huge_valf()) : (q < a.Lq ? delb[q] : 0.f);
-    }
-  };
-  fetch(0);
-  for (int t = 0; t < nq; ++t) {
-    const int qb = t * 64;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-      *(u32x4*)(Qs + offB(row, ch << 4)) = rq[i];
-      *(u32x4*)(Ds + offB(row, ch << 4)) = rd[i];
-    }
-    if (tid < 128) Ls[tid] = rl;
-    __syncthreads();
-    if (t + 1 < nq) fetch(qb + 64);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      f32x16 st, dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
-      const int row = qt * 32 + l32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        st = mfma32(*(const bf16x8*)(Qs + offB(row, (ks * 2 + hh) * 16)), kf[ks], st);
-        dpt = mfma32(*(const bf16x8*)(Ds + offB(row, (ks * 2 + hh) * 16)), vf[ks], dpt);
-      }
-      // rows q = qb + qt*32 + (r&3) + 8(r>>2) + 4hh
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int q4 = qt * 32 + 8 * rg + 4 * hh;
-        const f32x4 l4 = *(const f32x4*)(Ls + q4);
-        const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = kvalid ? __builtin_amdgcn_exp2f(st[rg * 4 + r] * a.sl2 - l4[r]) : 0.f;
-          st[rg * 4 + r] = p;
-          dpt[rg * 4 + r] = p * (dpt[rg * 4 + r] - d4[r]);
-        }
-      }
-      bf16x8 pk[2], dk8[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        pk[s2] = (bf16x8){f2bf(st[8 * s2 + 0]), f2bf(st[8 * s2 + 1]), f2bf(st[8 * s2 + 2]),
-                          f2bf(st[8 * s2 + 3]), f2bf(st[8 * s2 + 4]), f2bf(st[8 * s2 + 5]),
-                          f2bf(st[8 * s2 + 6]), f2bf(st[8 * s2 + 7])};
-        dk8[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                           f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                           f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int ra = qt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const bf16x8 dof = cat8(lds_read_tr(Ds + offB(ra, byte)), lds_read_tr(Ds + offB(ra + 8, byte)));
-          const bf16x8 qtf = cat8(lds_read_tr(Qs + offB(ra, byte)), lds_read_tr(Qs + offB(ra + 8, byte)));
-          dv[dt] = mfma32(dof, pk[s2], dv[dt]);
-          dk[dt] = mfma32(qtf, dk8[s2], dk[dt]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (key < a.Lk) {
-    bf16* dKb = a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk;
-    bf16* dVb = a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 vk, vv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          vk[r] = f2bf(dk[dt][rg * 4 + r] * a.scale);
-          vv[r] = f2bf(dv[dt][rg * 4 + r]);
-        }
-        *(bf16x4*)(dKb + dt * 32 + 8 * rg + 4 * hh) = vk;
-        *(bf16x4*)(dVb + dt * 32 + 8 * rg + 4 * hh) = vv;
-      }
-  }
-}
-
 // dK, dV with 8 waves (two per SIMD): 256 keys per workgroup, 32 per wave with the K^T
 // fragments and the dK^T / dV^T accumulators resident; V of the workgroup's keys is staged once
 // in LDS (the B operand of dP = dO.V^T is re-read per query slice) so a wave fits the 256
-// registers that two waves per SIMD allow.  Q / dO tiles of 64 queries and their LSE / D rows
-// arrive by LDS-DMA into a 2-stage ring, one barrier per tile: tile t+1 is issued at the top of
-// tile t into the stage tile t-1 used (all waves are past the barrier that ended tile t-1) and
-// retired by vmcnt(0) + the barrier that ends tile t.  Per-element arithmetic and its order are
-// those of attn_bwd_dkdv32_kernel (bit-identical results).
-__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_kernel(AttnBwdArgs a) {
+// registers that two waves per SIMD allow.  S = Q.K^T and dP = dO.V^T with the key on the lane,
+// so P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.  Q / dO tiles of
+// 64 queries and their LSE / D rows arrive by LDS-DMA into a 2-stage ring, one barrier per tile:
+// tile t+1 is issued at the top of tile t into the stage tile t-1 used (all waves are past the
+// barrier that ended tile t-1) and retired by vmcnt(0) + the barrier that ends tile t.
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   constexpr int V_BYTES = 256 * 256, STAGE = 16384 * 2 + 512;
   __shared__ __attribute__((aligned(16))) char smem[V_BYTES + 2 * STAGE];
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 256;
@@ -1846,6 +485,115 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_kernel(AttnBwdArgs a) {
   }
 }
 
+// dQ: 8 waves x 32 queries; per 96-key tile S^T = K.Q^T, dP^T = V.dO^T (query on the lane, so
+// LSE and D are per-lane scalars), dS^T = P^T (dP^T - D) packed to bf16, dQ^T += K^T dS^T.  The
+// K / V tiles arrive by LDS-DMA into a 2-stage ring (tile t+1 issued at the top of tile t,
+// retired by vmcnt(0) + the one barrier per tile).
+template <int NKT>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const bf16* Qb = a.Q + b * a.bq + h * HD;
+  const bf16* Kb = a.K + b * a.bk + h * HD;
+  const bf16* Vb = a.V + b * a.bv + h * HD;
+  const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+  bf16x8 qf[8], df[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
+    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
+  }
+  const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
+  const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
+  f32x16 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+  const int nkv = (a.k_len + TK - 1) / TK;
+  // K / V tile by LDS-DMA: 16 + 16 pieces of 4 rows, 2 + 2 per wave, swizzles on the source
+  auto dma = [&](int t, int st) {
+    char* Ks = smem + st * SB;
+    char* Vs = Ks + SV;
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+      const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+      const int kr = min(t * TK + row, a.Lk - 1);
+      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+      dma16(Kb + (int64_t)kr * a.ldk + ((pc ^ swzb) << 3), lds_addr(Ks + piece * 1024));
+      dma16(Vb + (int64_t)kr * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
+    }
+  };
+  dma(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
+  __syncthreads();
+  for (int t = 0; t < nkv; ++t) {
+    const int kb = t * TK;
+    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
+    if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
+    const char* Ks = smem + (t & 1) * SB;
+    const char* Vs = Ks + SV;
+    bf16x8 dsp[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+      const int row = kt * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
+        dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
+        dpt[r] = p * (dpt[r] - del);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
+          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  const int qo = q0 + w * 32 + l32;
+  if (qo < a.Lq) {
+    bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][rg * 4 + r] * a.scale);
+        *(bf16x4*)(dQb + dt * 32 + 8 * rg + 4 * hh) = v;
+      }
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
@@ -1858,50 +606,18 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || (ldq | ldk | ldv | ldo) % 8)
     return (int)hipErrorInvalidValue;
+  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535) return (int)hipErrorInvalidValue;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f, getenv("PRFL_ATTN_STAGGER") ? 1 : 0, nullptr};
-  static const int prio = getenv("PRFL_ATTN_PRIO") ? atoi(getenv("PRFL_ATTN_PRIO")) : 0;
+             scale * 1.4426950408889634f};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
-  static const int impl = getenv("PRFL_ATTN_FWD16") ? 16 : getenv("PRFL_ATTN_FWD32") ? 32
-                          : getenv("PRFL_ATTN_PP1") ? 2 : 3;
-  // default: pp3 (96-key tiles) at SCHED 2; PRFL_ATTN_NKT=2 selects pp2 (64-key tiles, SCHED 1)
-  static const int nkt = getenv("PRFL_ATTN_NKT") ? atoi(getenv("PRFL_ATTN_NKT")) : 3;
-  static const int sched = getenv("PRFL_ATTN_SCHED") ? atoi(getenv("PRFL_ATTN_SCHED"))
-                                                      : (nkt == 3 ? 2 : 1);
-  const dim3 g2((Lq + 255) / 256, H, B);
-  if (impl == 3 && nkt == 3) {
-    a.stagger = prio;   // pp3 reads it as the priority mode
-    if (kid != KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp3_kernel<true, 1, 3>), g2, dim3(512), 0, s, a);
-    else if (sched == 0) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 0, 3>), g2, dim3(512), 0, s, a);
-    else if (sched == 2) hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 2, 3>), g2, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_pp3_kernel<false, 1, 3>), g2, dim3(512), 0, s, a);
-  } else if (impl == 3 && sched == 1) {
-    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 1>), g2, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 1>), g2, dim3(512), 0, s, a);
-  } else if (impl == 3 && sched == 3) {
-    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 3>), g2, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 3>), g2, dim3(512), 0, s, a);
-  } else if (impl == 3) {
-    if (kid == KID_ATTN_FWD) hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 0>), g2, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_pp2_kernel<true, 0>), g2, dim3(512), 0, s, a);
-  } else if (impl == 2) {
-    if (kid == KID_ATTN_FWD)
-      hipLaunchKernelGGL(attn_fwd_pp_kernel<false>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL(attn_fwd_pp_kernel<true>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
-  } else if (impl == 32) {
-    if (kid == KID_ATTN_FWD)
-      hipLaunchKernelGGL(attn_fwd32_kernel<false>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL(attn_fwd32_kernel<true>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
-  } else if (kid == KID_ATTN_FWD) {
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
-  }
+  const dim3 grid((Lq + 255) / 256, H, B);
+  if (kid == KID_ATTN_FWD)
+    hipLaunchKernelGGL((attn_fwd_kernel<false, 2, 3>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3>), grid, dim3(512), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();
@@ -1918,6 +634,11 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                              int64_t k_len, float scale, void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
+      !aligned16(dq) || !aligned16(dk) || !aligned16(dv) ||
+      (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8)
+    return (int)hipErrorInvalidValue;
+  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrows = B * Lq * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((nrows + 15) / 16), dim3(256), 0, s,
@@ -1928,46 +649,15 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
                 scale * 1.4426950408889634f, scale};
-  static const bool bwd16 = getenv("PRFL_ATTN_BWD16") != nullptr;
-  static const bool dkdv4 = getenv("PRFL_ATTN_DKDV4") != nullptr;
-  static const bool dq32old = getenv("PRFL_ATTN_DQ32") != nullptr;
-  static const bool dqw3 = getenv("PRFL_ATTN_DQ64") == nullptr;   // default: 96-key K/V tiles
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
-  if (bwd16)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
-  else if (dkdv4)
-    hipLaunchKernelGGL(attn_bwd_dkdv32_kernel, dim3((Lk + 127) / 128, H, B), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv8_kernel, dim3((Lk + 255) / 256, H, B), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 255) / 256, H, B), dim3(512), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();
   prfl_prof::begin(KID_ATTN_BWD_DQ, s);
-  if (bwd16)
-    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((Lq + 127) / 128, H, B), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(dq32old ? attn_bwd_dq32_kernel
-                       : dqw3 ? attn_bwd_dq8w_kernel<3> : attn_bwd_dq8_kernel, dim3((Lq + 255) / 256, H, B),
-                       dim3(512), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
-  PRFL_LAUNCH_CHECK();
-  return 0;
-}
-
-// Diagnostic build of the self-attention forward (attn_fwd_pp2_kernel with cycle stamps): per wave
-// of workgroups (x < 16, head 0, batch 0), stamps[(x*8 + wave)*4 + {0..3}] = summed cycles of
-// {MFMA phase, barrier wait after it, softmax phase, barrier wait after it}.  Read the SHARES, not
-// the run time (the stamps' lgkmcnt(0) fences change the schedule).  Not used by the product path.
-extern "C" int prfl_attn_fwd_stamped(const void* q, int64_t ldq, const void* k, int64_t ldk,
-                                     const void* v, int64_t ldv, void* o, int64_t ldo, float* lse2,
-                                     int64_t L, int64_t H, float scale,
-                                     unsigned long long* stamps, void* stream) {
-  if (L < 4096 || H <= 0) return (int)hipErrorInvalidValue;
-  AttnArgs a{(const bf16*)q, ldq, 0, (const bf16*)k, ldk, 0, (const bf16*)v, ldv, 0, (bf16*)o, ldo,
-             0, lse2, (int)L, (int)L, (int)H, (int)L, scale * 1.4426950408889634f, 0, stamps};
-  hipLaunchKernelGGL((attn_fwd_pp2_kernel<false, 1, true>), dim3((L + 255) / 256, H, 1), dim3(512),
-                     0, (hipStream_t)stream, a);
   PRFL_LAUNCH_CHECK();
   return 0;
 }

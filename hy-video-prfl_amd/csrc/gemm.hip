@@ -279,51 +279,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
 
 // =========================================================================== 256x256 tile ===
 // 8 waves (2 along M x 4 along N), each 128x64 = 8x4 MFMA 16x16x32 tiles; BK = 64; operands
-// land in LDS by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece per wave instruction) into a
-// 2-deep ring (2 x 64 KiB).  Tile t+1 stays in flight across the barriers while tile t computes
-// (counted `s_waitcnt vmcnt(8)` + raw s_barrier; no __syncthreads in the loop, one __shared__
-// array), per MI355X guide §5 "Pipelining across barriers".  The LDS images are the same
-// swizzled layouts as above, produced by permuting each lane's SOURCE address (the DMA
-// destination is lane-linear).  Requires K % 64 == 0 and MN-major extents % 256 == 0.
+// land in LDS by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece per wave instruction) and
+// stay in flight across the barriers (counted `s_waitcnt vmcnt(N)` + raw s_barrier; no
+// __syncthreads in the loop, one __shared__ array), per MI355X guide §5 "Pipelining across
+// barriers".  The LDS images are the swizzled layouts above, produced by permuting each lane's
+// SOURCE address (the DMA destination is lane-linear).  Requires K % 64 == 0 and MN-major
+// extents % 256 == 0.
 constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
 constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
 
-
-template <bool KC>
-__device__ __forceinline__ void dma_tile(char* lds, const bf16* __restrict__ P, int64_t ld, int rows,
-                                         int r0, int k0, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wid * 4 + i;                     // 32 pieces of 1 KiB
-    const bf16* src;
-    if (KC) {          // piece = 8 rows x 128 B; lane -> (row, physical chunk)
-      const int row = piece * 8 + (lane >> 3), pc = lane & 7;
-      const int gr = min(r0 + row, rows - 1);
-      src = P + (int64_t)gr * ld + k0 + ((pc ^ (row & 7)) << 3);
-    } else {           // piece = 2 k-rows x 512 B
-      const int kr = piece * 2 + (lane >> 5), pb = (lane & 31) << 4;
-      const int lb = pb ^ (swz_mn(kr) << 5);
-      src = P + (int64_t)(k0 + kr) * ld + r0 + (lb >> 1);
-    }
-    dma16(src, lds_addr(lds + piece * 1024));
-  }
-}
-
-template <bool KC>
-__device__ __forceinline__ bf16x8 read_frag2(const char* lds, int base, int s, int lane) {
-  if (KC) {
-    const int row = base + (lane & 15);
-    const int kc = s * 4 + (lane >> 4);
-    return *(const bf16x8*)(lds + row * 128 + ((kc ^ (row & 7)) << 4));
-  } else {
-    const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
-    const int col = (base + 4 * p) * 2;
-    const int k0 = s * 32 + g * 8 + q, k1 = k0 + 4;
-    bf16x4 lo = lds_read_tr(lds + k0 * 512 + (col ^ (swz_mn(k0) << 5)));
-    bf16x4 hi = lds_read_tr(lds + k1 * 512 + (col ^ (swz_mn(k1) << 5)));
-    return cat8(lo, hi);
-  }
-}
 
 __device__ __forceinline__ void tile_coords2(int bid, int M, int N, int& tm, int& tn) {
   const int ntm = (M + BM2 - 1) / BM2, ntn = (N + BN2 - 1) / BN2;
@@ -339,75 +303,8 @@ __device__ __forceinline__ void tile_coords2(int bid, int M, int N, int& tm, int
   tn = within / gsz;
 }
 
-template <bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A|B]
-  int tm, tn;
-  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = g.K / BK;
-  dma_tile<A_KC>(smem, g.A, g.lda, g.M, m0, 0, wid, lane);
-  dma_tile<B_KC>(smem + TILE2, g.B, g.ldb, g.N, n0, 0, wid, lane);
-  if (nk > 1) {
-    dma_tile<A_KC>(smem + 2 * TILE2, g.A, g.lda, g.M, m0, BK, wid, lane);
-    dma_tile<B_KC>(smem + 3 * TILE2, g.B, g.ldb, g.N, n0, BK, wid, lane);
-  }
-  for (int t = 0; t < nk; ++t) {
-    // tile t landed (8 DMA instructions per wave per tile; tile t+1 may stay in flight)
-    if (t + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* As = smem + (t & 1) * 2 * TILE2;
-    const char* Bs = As + TILE2;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 bf[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = read_frag2<B_KC>(Bs, wc * 64 + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 af = read_frag2<A_KC>(As, wr * 128 + i * 16, s, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bf[j], af, acc[i][j]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                     // every wave is done reading stage t&1
-    asm volatile("" ::: "memory");
-    if (t + 2 < nk) {
-      char* st = smem + (t & 1) * 2 * TILE2;
-      dma_tile<A_KC>(st, g.A, g.lda, g.M, m0, (t + 2) * BK, wid, lane);
-      dma_tile<B_KC>(st + TILE2, g.B, g.ldb, g.N, n0, (t + 2) * BK, wid, lane);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= g.N) continue;
-      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
-    }
-  }
-}
-
 // ------------------------------------------------------------ 256x256, staggered 4-phase ---
-// Same tile and wave grid as gemm256_kernel, re-scheduled after the MI355X guide's 8-phase
+// The 256x256 tile and 8-wave grid above, scheduled after the MI355X guide's 8-phase
 // template (cdna_hip_programming.md §5): every K-tile is four phases, one C-quadrant (16 MFMAs)
 // each; a phase = {fragment reads for its quadrant + one half-tile LDS-DMA} | barrier |
 // {lgkmcnt(0), MFMA cluster, counted vmcnt} | barrier.  Waves 4-7 (wr = 1) run one barrier
@@ -416,9 +313,15 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs g) {
 //   A_h0: rows wr*128 + {0..63}   (quadrants 0, 1)    B_h0: cols wc*64 + {0..31}  (quadrants 0, 2)
 //   A_h1: rows wr*128 + {64..127} (quadrants 2, 3)    B_h1: cols wc*64 + {32..63} (quadrants 1, 3)
 // Half-tile h (tile h/4, part order A_h0, B_h0, B_h1, A_h1) is issued in phase h-6 into a 2-deep
-// ring and retired by the counted vmcnt at the end of phase h-3; a slot is re-filled >= 2
-// phases after its last read (>= 1 for the lagging half), which the stagger's barrier order
-// makes safe (the guide's 'Read a staged buffer one phase AFTER the wait that retires it').
+// ring, retired by the counted vmcnt at the end of phase h-3 and first read in phase h-1 (A_h0:
+// phase h).  Barrier numbering: wave group wr runs phase k between barriers 2k+1+wr and
+// 2k+2+wr, so a writer of group wr retires h before barrier 2h-4+wr and a reader of group wr'
+// reads it after barrier 2h-2+wr' >= 2h-3: every half-tile is retired by BOTH groups one
+// barrier before its first reader passes (the guide's 'Read a staged buffer one phase AFTER
+// the wait that retires it', with the stagger's extra barrier).  Half-tiles 0-2 are read in
+// phases 0-1, before any in-loop wait: the prologue must retire all three (round 1 retired only
+// 0-1, so waves 0-3 could read waves 4-7's half of B_h1 of tile 0 before it landed).  WAR: a
+// slot is re-filled in phase h-6, >= 2 phases after its last read (phase h-8).
 constexpr int HALF = 16384;
 
 template <bool KC, bool IS_A>
@@ -474,10 +377,11 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
     if (part == 1) dma_half<B_KC, false>(st + 2 * HALF, g.B, g.ldb, g.N, n0, T * BK, 0, wid, lane);
     if (part == 2) dma_half<B_KC, false>(st + 3 * HALF, g.B, g.ldb, g.N, n0, T * BK, 1, wid, lane);
   };
-  const int pro = min(6, nph);
+  const int pro = min(6, nph);           // nph % 4 == 0: pro is 4 or 6 half-tiles
   for (int h = 0; h < pro; ++h) issue(h >> 2, h & 3);
-  if (pro == 6) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  // retire half-tiles 0, 1, 2 (2 DMA instructions per wave each); leave the rest in flight
+  if (pro == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -590,17 +494,16 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
   }
 }
 
+// tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced
+// (parity tests: both kernels accumulate every element in the same k order, so their outputs
+// are bit-identical)
 template <bool A_KC, bool B_KC, int EPI>
-int launch(const GemmArgs& g, hipStream_t s) {
-  static const bool no256 = getenv("PRFL_GEMM128") != nullptr;
+int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
-  const bool ok256 = !no256 && (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) &&
-                     (B_KC || g.N % BN2 == 0) && nt256 >= 96;
-  static const bool nostagger = getenv("PRFL_GEMM_NOSTAGGER") != nullptr;
-  if (ok256 && !nostagger) {
+  const bool fits256 = (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) && (B_KC || g.N % BN2 == 0);
+  if (tile == 256 && !fits256) return (int)hipErrorInvalidValue;
+  if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
     hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
-  } else if (ok256) {
-    hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
   } else {
     const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
     hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);
@@ -611,12 +514,14 @@ int launch(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
-                              int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                              int epilogue, const void* bias, const float* gate, const void* res,
-                              int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
-                              void* stream) {
+extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, const void* B,
+                                    int64_t ldb, int b_kmajor, void* C, int64_t ldc, int64_t M,
+                                    int64_t N, int64_t K, int epilogue, const void* bias,
+                                    const float* gate, const void* res, int64_t ldr, int res_bf16,
+                                    void* aux, int64_t ldaux, int accumulate, int tile,
+                                    void* stream) {
   if (M <= 0 || N <= 0) return 0;
+  if (tile != 0 && tile != 128 && tile != 256) return (int)hipErrorInvalidValue;
   // K is a contiguous extent only for K-major operands; MN-major operands take any K (row tail)
   if (K <= 0 || ((a_kmajor || b_kmajor) && (K % 8) != 0) || (N % 4) != 0)
     return (int)hipErrorInvalidValue;
@@ -632,12 +537,12 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
   int rc = (int)hipErrorInvalidValue;
   // weight gradients with a token count K that is not a multiple of 64: the bulk of K goes
   // through the 256-tile kernel, the < 64-row tail is accumulated by a second (128-tile) launch
-  if (epilogue == EPI_F32 && !a_kmajor && !b_kmajor && (K % BK) != 0 && K > BK &&
+  if (tile != 128 && epilogue == EPI_F32 && !a_kmajor && !b_kmajor && (K % BK) != 0 && K > BK &&
       (M % BM2) == 0 && (N % BN2) == 0) {
     const int64_t Kmain = K - K % BK;
     GemmArgs gm = g;
     gm.K = (int)Kmain;
-    rc = launch<false, false, EPI_F32>(gm, s);
+    rc = launch<false, false, EPI_F32>(gm, s, tile);
     if (rc == 0) {
       GemmArgs gt = g;
       gt.A = g.A + Kmain * lda;
@@ -653,7 +558,7 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
     return rc;
   }
 #define GEMM_CASE(AK, BK_, E) \
-  if (a_kmajor == AK && b_kmajor == BK_ && epilogue == E) rc = launch<AK, BK_, E>(g, s);
+  if (a_kmajor == AK && b_kmajor == BK_ && epilogue == E) rc = launch<AK, BK_, E>(g, s, tile);
   GEMM_CASE(1, 1, EPI_BF16)
   GEMM_CASE(1, 1, EPI_GELU)
   GEMM_CASE(1, 1, EPI_RESID)
@@ -670,115 +575,24 @@ extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const vo
   return rc;
 }
 
+extern "C" int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+                              int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                              int epilogue, const void* bias, const float* gate, const void* res,
+                              int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
+                              void* stream) {
+  return prfl_gemm_bf16_tiled(A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, M, N, K, epilogue, bias,
+                              gate, res, ldr, res_bf16, aux, ldaux, accumulate, 0, stream);
+}
+
 // ================================================================ fp8 (C5: I2V 720p fp8 path) ===
 // C[m][n] = sa[m] * sb[n] * sum_k A8(m,k) B8(n,k)   (+ the bf16 kernel's epilogues)
 // A8 / B8 are OCP e4m3 (gfx950 `e4m3fn`), both K-major, quantised per row (prfl_quant_rows_fp8).
 // The MFMA is the block-scaled `v_mfma_scale_f32_16x16x128_f8f6f4` (2x the bf16 MFMA rate; the
 // unscaled fp8 forms run at the bf16 rate) with every E8M0 block scale = 2^0: the per-row /
 // per-column dequantisation happens once, in fp32, in the epilogue.
-// Same 256x256 tile, 8-wave grid and 2-deep LDS-DMA ring as gemm256_kernel; BK = 128 fp8 = 128 B
-// per row, so the swizzled LDS image (128-B rows, 16-B chunk ^ (row & 7)) is byte-identical to
-// the bf16 kernel's; each lane's fragment is 32 consecutive k (two 16-B chunks).
+// It runs on gemm256s_kernel<.., F8 = true>: the staggered bf16 schedule over the same BYTES (an
+// e4m3 [rows][K] operand passed as bf16 [rows][K/2]).
 namespace {
-constexpr int BK8 = 128;
-
-struct ScaleArgs {
-  const float* sa;   // [M]
-  const float* sb;   // [N]
-};
-
-__device__ __forceinline__ void dma_tile8(char* lds, const uint8_t* __restrict__ P, int64_t ld,
-                                          int rows, int r0, int k0, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wid * 4 + i;                     // 32 pieces of 1 KiB = 8 rows x 128 B
-    const int row = piece * 8 + (lane >> 3), pc = lane & 7;
-    const int gr = min(r0 + row, rows - 1);
-    dma16(P + (int64_t)gr * ld + k0 + ((pc ^ (row & 7)) << 4), lds_addr(lds + piece * 1024));
-  }
-}
-
-// lane l: X[row = base + (l&15)][k = 32*(l>>4) + 0..31] (chunks 2g, 2g+1 of the 128-B row)
-__device__ __forceinline__ i32x8 read_frag8(const char* lds, int base, int lane) {
-  const int row = base + (lane & 15);
-  const int c0 = 2 * (lane >> 4);
-  const u32x4 lo = *(const u32x4*)(lds + row * 128 + ((c0 ^ (row & 7)) << 4));
-  const u32x4 hi = *(const u32x4*)(lds + row * 128 + (((c0 + 1) ^ (row & 7)) << 4));
-  return (i32x8){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3],
-                 (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-}
-
-
-template <int EPI>
-__global__ __launch_bounds__(NT2, 1) void gemm256_fp8_kernel(GemmArgs g, ScaleArgs sc) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE2];   // [stage][A|B], 32 KiB each
-  int tm, tn;
-  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const uint8_t* A = (const uint8_t*)g.A;
-  const uint8_t* B = (const uint8_t*)g.B;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = g.K / BK8;
-  dma_tile8(smem, A, g.lda, g.M, m0, 0, wid, lane);
-  dma_tile8(smem + TILE2, B, g.ldb, g.N, n0, 0, wid, lane);
-  if (nk > 1) {
-    dma_tile8(smem + 2 * TILE2, A, g.lda, g.M, m0, BK8, wid, lane);
-    dma_tile8(smem + 3 * TILE2, B, g.ldb, g.N, n0, BK8, wid, lane);
-  }
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* As = smem + (t & 1) * 2 * TILE2;
-    const char* Bs = As + TILE2;
-    i32x8 bf[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = read_frag8(Bs, wc * 64 + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const i32x8 af = read_frag8(As, wr * 128 + i * 16, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_fp8(bf[j], af, acc[i][j]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 2 < nk) {
-      char* st = smem + (t & 1) * 2 * TILE2;
-      dma_tile8(st, A, g.lda, g.M, m0, (t + 2) * BK8, wid, lane);
-      dma_tile8(st + TILE2, B, g.ldb, g.N, n0, (t + 2) * BK8, wid, lane);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    const float s_m = sc.sa[m];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= g.N) continue;
-      const f32x4 s_n = *(const f32x4*)(sc.sb + n);
-      f32x4 v = acc[i][j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = v[r] * (s_m * s_n[r]);
-      epilogue_tile<true, true, EPI>(g, v, m, n);
-    }
-  }
-}
-
 // ---- per-row e4m3 quantisation: scale[m] = amax_m / 448, q = e4m3(x * (448 / amax_m)) ------
 constexpr int QNT = 256, QMAXC = 8;     // <= 8 chunks of 8 per thread: K <= 16384
 constexpr float E4M3_MAX = 448.f;
@@ -856,7 +670,7 @@ extern "C" int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const 
                              const float* gate, const void* res, int64_t ldr, int res_bf16,
                              void* aux, int64_t ldaux, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (K <= 0 || K % BK8 || N % 4 || lda % 16 || ldb % 16 || ((uintptr_t)A & 15) ||
+  if (K <= 0 || K % 128 || N % 4 || lda % 16 || ldb % 16 || ((uintptr_t)A & 15) ||
       ((uintptr_t)B & 15) || ((uintptr_t)sb & 15) || !sa || !sb)
     return (int)hipErrorInvalidValue;
   if (M > 0x7fffffff || N > 0x7fffffff || K > 0x7fffffff) return (int)hipErrorInvalidValue;
@@ -864,31 +678,22 @@ extern "C" int prfl_gemm_fp8(const void* A, int64_t lda, const float* sa, const 
     return (int)hipErrorInvalidValue;
   GemmArgs g{(const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, (int)M, (int)N, (int)K,
              (const bf16*)bias, gate, res, ldr, res_bf16, (bf16*)aux, ldaux, 0};
-  ScaleArgs sc{sa, sb};
   hipStream_t s = (hipStream_t)stream;
   const int nt = (int)(((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2));
-  static const bool simple = getenv("PRFL_FP8_SIMPLE") != nullptr;
   prfl_prof::begin(KID_GEMM, s);
-  if (!simple) {
-    // the staggered 4-phase bf16 schedule over the same bytes: K8 e4m3 = K8/2 "bf16" columns
-    GemmArgs g2 = g;
-    g2.lda = lda / 2;
-    g2.ldb = ldb / 2;
-    g2.K = (int)(K / 2);
-    g2.sa = sa;
-    g2.sb = sb;
-    if (epilogue == EPI_BF16)
-      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_BF16, true>), dim3(nt), dim3(NT2), 0, s, g2);
-    else if (epilogue == EPI_GELU)
-      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_GELU, true>), dim3(nt), dim3(NT2), 0, s, g2);
-    else
-      hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_RESID, true>), dim3(nt), dim3(NT2), 0, s, g2);
-  } else if (epilogue == EPI_BF16)
-    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_BF16>, dim3(nt), dim3(NT2), 0, s, g, sc);
+  // the staggered 4-phase bf16 schedule over the same bytes: K8 e4m3 = K8/2 "bf16" columns
+  GemmArgs g2 = g;
+  g2.lda = lda / 2;
+  g2.ldb = ldb / 2;
+  g2.K = (int)(K / 2);
+  g2.sa = sa;
+  g2.sb = sb;
+  if (epilogue == EPI_BF16)
+    hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_BF16, true>), dim3(nt), dim3(NT2), 0, s, g2);
   else if (epilogue == EPI_GELU)
-    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_GELU>, dim3(nt), dim3(NT2), 0, s, g, sc);
+    hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_GELU, true>), dim3(nt), dim3(NT2), 0, s, g2);
   else
-    hipLaunchKernelGGL(gemm256_fp8_kernel<EPI_RESID>, dim3(nt), dim3(NT2), 0, s, g, sc);
+    hipLaunchKernelGGL((gemm256s_kernel<true, true, EPI_RESID, true>), dim3(nt), dim3(NT2), 0, s, g2);
   prfl_prof::set_work(2.0 * (double)M * (double)N * (double)K);
   prfl_prof::end(KID_GEMM, s);
   PRFL_LAUNCH_CHECK();

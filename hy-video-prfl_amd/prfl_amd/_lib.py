@@ -19,9 +19,10 @@ F32 = ctypes.c_float
 SIGNATURES = {
     "prfl_gemm_bf16": [P, I64, I32, P, I64, I32, P, I64, I64, I64, I64, I32, P, P, P, I64, I32, P,
                        I64, I32, P],
+    "prfl_gemm_bf16_tiled": [P, I64, I32, P, I64, I32, P, I64, I64, I64, I64, I32, P, P, P, I64,
+                             I32, P, I64, I32, I32, P],
     "prfl_attn_fwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
                       I64, F32, P],
-    "prfl_attn_fwd_stamped": [P, I64, P, I64, P, I64, P, I64, P, I64, I64, F32, P, P],
     "prfl_attn_bwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64,
                       I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],

@@ -20,28 +20,29 @@ def _ld(t):
 
 
 def gemm(a, b, c, M, N, K, a_kmajor=True, b_kmajor=True, epilogue=EPI_BF16, bias=None,
-         gate=None, res=None, aux=None, accumulate=False):
-    """C[m][n] = sum_k A(m,k) B(n,k) (+ epilogue); see include/prfl_hip.h."""
+         gate=None, res=None, aux=None, accumulate=False, tile=0):
+    """C[m][n] = sum_k A(m,k) B(n,k) (+ epilogue); see include/prfl_hip.h.  tile: 0 = by shape,
+    128 / 256 = forced (prfl_gemm_bf16_tiled)."""
     _lib.require_gpu(a, b, c)
     assert a.dtype == BF16 and b.dtype == BF16
     assert bias is None or (bias.dtype == BF16 and bias.is_contiguous())
     assert gate is None or (gate.dtype == torch.float32 and gate.is_contiguous())
-    call("prfl_gemm_bf16", ptr(a), I64(_ld(a)), I32(int(a_kmajor)), ptr(b), I64(_ld(b)),
+    call("prfl_gemm_bf16_tiled", ptr(a), I64(_ld(a)), I32(int(a_kmajor)), ptr(b), I64(_ld(b)),
          I32(int(b_kmajor)), ptr(c), I64(_ld(c)), I64(M), I64(N), I64(K), I32(epilogue),
          ptr(bias), ptr(gate), ptr(res), I64(_ld(res) if res is not None else 0),
          I32(int(res is not None and res.dtype == BF16)), ptr(aux),
-         I64(_ld(aux) if aux is not None else 0), I32(int(accumulate)), stream_ptr())
+         I64(_ld(aux) if aux is not None else 0), I32(int(accumulate)), I32(tile), stream_ptr())
     return c
 
 
-def linear(x, w, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None, aux=None):
+def linear(x, w, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None, aux=None, tile=0):
     """y = x @ w^T (+bias) with x [M,K] bf16, w [N,K] bf16 (nn.Linear layout)."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         dt = torch.float32 if epilogue in (EPI_RESID, EPI_F32) else BF16
         out = torch.empty(M, N, dtype=dt, device=x.device)
-    return gemm(x, w, out, M, N, K, True, True, epilogue, bias, gate, res, aux)
+    return gemm(x, w, out, M, N, K, True, True, epilogue, bias, gate, res, aux, tile=tile)
 
 
 def linear_dx(dy, w, out=None, epilogue=EPI_BF16, aux=None):

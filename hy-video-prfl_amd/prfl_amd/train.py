@@ -138,10 +138,18 @@ class PRFLTrainer:
 
 
 class PAVRMTrainer:
-    """train_pavrm.py:671-920 with loss 'ce': BCE(sigmoid(MLP(QA(features))), label)."""
+    """train_pavrm.py:671-920 with loss 'ce': BCE(sigmoid(MLP(QA(features))), label).
 
-    def __init__(self, lrm, query_attention, mlp, lr=1e-6, lr_head=1e-5, weight_decay=0.01,
-                 flow_shift=5.0, feature_layer=(8,)):
+    Optimizer = `optimizer_init` (`train_pavrm.py:459-506`): the transformer's trainable blocks at
+    `lr`; the MLP and QueryAttention at `lr_head` = `learning_rate_mlp` when the config sets it,
+    else `lr` (the CE configs leave it commented out, `train_pavrm_t2v_480.yaml:61-62`).  One
+    AdamW over the three groups is the same update as one AdamW per group (AdamW is per
+    parameter).  Clipping = `transformer.clip_grad_norm_(1.0)` after backward (`:899`) over the
+    transformer grads only; the pre-backward clip of `:883-889` runs on parameters whose grads
+    were cleared by the previous `zero_grad`, so it clips nothing and is not restated."""
+
+    def __init__(self, lrm, query_attention, mlp, lr=1e-6, lr_head=None, weight_decay=0.01,
+                 flow_shift=5.0, feature_layer=(8,), max_grad_norm=1.0):
         self.lrm, self.qa, self.mlp = lrm, query_attention, mlp
         for p in lrm.parameters():
             p.requires_grad_(False)
@@ -152,21 +160,30 @@ class PAVRMTrainer:
             for p in m.parameters():
                 p.requires_grad_(True)
         self.trunk_params = [p for p in lrm.parameters() if p.requires_grad]
-        self.head_params = list(query_attention.parameters()) + list(mlp.parameters())
+        self.head_params = list(mlp.parameters()) + list(query_attention.parameters())
+        lr_head = lr if lr_head is None else lr_head
         self.opt_trunk = AdamW(self.trunk_params, lr=lr, weight_decay=weight_decay)
         self.opt_head = AdamW(self.head_params, lr=lr_head, weight_decay=weight_decay)
         self.reducer = GradReducer(self.trunk_params + self.head_params)
         self.fm = FlowMatchDiscreteScheduler(shift=flow_shift)
         self.fm.set_timesteps(1000, dtype=torch.int64)
         self.feature_layer = list(feature_layer)
+        self.max_grad_norm = max_grad_norm
 
     def step(self, latents, text_states, seq_len, label, image_embeds=None, cond=None,
-             generator=None):
+             generator=None, noise=None, timestep=None):
+        """One PAVRM step; `noise` / `timestep` (values of the 1000-step schedule's `timesteps`,
+        as `train_pavrm.py:721-728` passes them) replace the random draws when given."""
         bsz = latents.shape[0]
-        noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
-                            device=latents.device)
-        timestep, sigma = self.fm.get_train_timestep_and_sigma(
-            weighting_scheme="uniform", batch_size=bsz, device=latents.device, n_dim=latents.ndim)
+        if noise is None:
+            noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                                device=latents.device)
+        if timestep is None:
+            timestep, sigma = self.fm.get_train_timestep_and_sigma(
+                weighting_scheme="uniform", batch_size=bsz, device=latents.device,
+                n_dim=latents.ndim)
+        else:
+            sigma = self.fm.get_train_sigma(timestep, n_dim=latents.ndim, device=latents.device)
         noisy = self.fm.add_noise(latents, noise, sigma)
         feats = list2batch(self.lrm(x=batch2list(noisy), t=timestep, context=batch2list(text_states),
                                     seq_len=seq_len, clip_fea=image_embeds,
@@ -177,10 +194,9 @@ class PAVRMTrainer:
         self.reducer.begin()
         loss.backward()
         self.reducer.end()
-        grad_norm = clip_grad_norm_(self.trunk_params, 1.0)
-        clip_grad_norm_(self.head_params, 1.0)
+        grad_norm = clip_grad_norm_(self.trunk_params, self.max_grad_norm)
         self.opt_trunk.step()
         self.opt_head.step()
         self.opt_trunk.zero_grad()
         self.opt_head.zero_grad()
-        return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm)
+        return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm, prob=out.detach())

@@ -43,6 +43,15 @@ int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int6
                    int epilogue, const void* bias, const float* gate, const void* res,
                    int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
                    void* stream);
+/* The same GEMM with the tile chosen by the caller: tile = 0 (by shape, as prfl_gemm_bf16),
+ * 128 (128x128 tile, 4 waves) or 256 (256x256 tile, 8 waves, staggered LDS-DMA ring; needs
+ * K % 64 == 0 and MN-major extents % 256 == 0, else hipErrorInvalidValue).  Both kernels sum
+ * every output element in the same k order, so their results are bit-identical. */
+int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+                         int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                         int epilogue, const void* bias, const float* gate, const void* res,
+                         int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
+                         int tile, void* stream);
 
 /* ---- attention ---------------------------------------------------------------------------
  * Replaces flash_attn.flash_attn_varlen_func at diffusers_lite/wan/modules/attention.py:96-127
@@ -54,11 +63,6 @@ int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                   const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
                   float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
                   float scale, void* stream);
-/* Diagnostic only (not on the product path): the self-attention forward with in-kernel cycle
- * stamps of its two phases and barrier waits, for tools/attn_stamps.py. */
-int prfl_attn_fwd_stamped(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
-                          int64_t ldv, void* o, int64_t ldo, float* lse2, int64_t L, int64_t H,
-                          float scale, unsigned long long* stamps, void* stream);
 /* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
  * caller-owned workspace. */
 int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,

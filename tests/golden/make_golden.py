@@ -289,8 +289,69 @@ def case_toy_prfl():
         sft_loss=np32(sft_loss), **g_reward, **g_sft)
 
 
+def case_toy_pavrm():
+    """Toy PAVRM training step with the 'ce' loss, restating `train_pavrm.py:671-920` on the
+    reference modules: `model_init` (`:200-235`: embeddings frozen, trainable_blocks kept, head
+    dropped), `optimizer_init` (`:459-506`: ONE AdamW over three parameter groups — transformer,
+    MLP, QueryAttention — all at `learning_rate` because the CE configs leave
+    `learning_rate_mlp` commented out, `train_pavrm_t2v_480.yaml:61-62`), then per step: noise at
+    a fixed timestep, 8-block-style feature tap, 4-D QueryAttention pooling (`:793-800`, the
+    sp_size > 1 branch our DP run takes), sigmoid MLP, BCE (`:869`), the pre-backward clip that
+    sees no gradients (`:883-889`), backward, `transformer.clip_grad_norm_(1.0)` over the
+    transformer grads only (`:899`), optimizer.step, zero_grad.  Two steps, so the second one
+    runs on AdamW-updated weights with non-zero moments."""
+    lrm = _toy_model("t2v")
+    for name in ("patch_embedding", "text_embedding", "time_embedding", "time_projection"):
+        for p in getattr(lrm, name).parameters():
+            p.requires_grad_(False)
+    for blk in lrm.blocks:                                   # trainable_blocks [0, 1]
+        for p in blk.parameters():
+            p.requires_grad_(True)
+    del lrm.head
+    lrm.head = None
+    qa = load_seeded(NET.QueryAttention(256, 1, 8, 0., return_type="query"), prefix="pqa.")
+    mlp = load_seeded(NET.MLP(256), prefix="pmlp.")
+    tparams = [p for p in lrm.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW([{"params": tparams, "lr": 1e-6},
+                             {"params": list(mlp.parameters()), "lr": 1e-6},
+                             {"params": list(qa.parameters()), "lr": 1e-6}],
+                            betas=(0.9, 0.999), weight_decay=0.01, eps=1e-8)
+    fm = FM.FlowMatchDiscreteScheduler(shift=5.0)
+    fm.set_timesteps(1000, dtype=torch.int64)
+    crit = torch.nn.BCELoss()
+    ctx = torch.from_numpy(seeded.randn("pavrm.ctx", (1, 20, TOY["text_dim"]))).to(torch.bfloat16)
+    out = {"ctx": np32(ctx)}
+    for s, (idx, label) in enumerate(((613, 1.0), (287, 0.0))):
+        x0 = torch.from_numpy(seeded.randn(f"pavrm.x0.{s}", (1,) + TOY_LATENT)).to(torch.bfloat16)
+        noise = torch.from_numpy(seeded.randn(f"pavrm.noise.{s}", (1,) + TOY_LATENT)).to(torch.bfloat16)
+        timestep = fm.timesteps[[idx]]
+        sigma = fm.sigmas[[idx]].float().view(1, 1, 1, 1, 1)
+        noisy = fm.add_noise(x0, noise, sigma)
+        with torch.autocast(**AC):
+            feats = DU.list2batch(lrm(x=DU.batch2list(noisy), t=timestep, context=DU.batch2list(ctx),
+                                      seq_len=105, output_features=True, selected_layers=[2]))
+            pooled = qa(feats)
+            prob = NET.forward_mlp(mlp, pooled)
+        lab = torch.tensor([label])
+        loss = crit(prob.squeeze().float(), lab.squeeze().float())
+        loss.backward()
+        g = {f"s{s}:" + k: v for k, v in grads_of(lrm).items()}
+        g.update({f"s{s}:qa." + k: v for k, v in grads_of(qa).items()})
+        g.update({f"s{s}:mlp." + k: v for k, v in grads_of(mlp).items()})
+        gn = torch.nn.utils.clip_grad_norm_(tparams, max_norm=1.0)
+        opt.step()
+        opt.zero_grad()
+        out.update({f"s{s}:x0": np32(x0), f"s{s}:noise": np32(noise), f"s{s}:idx": np.int64(idx),
+                    f"s{s}:label": np.float32(label), f"s{s}:feat": np32(feats),
+                    f"s{s}:prob": np32(prob), f"s{s}:loss": np32(loss),
+                    f"s{s}:grad_norm": np32(gn), **g})
+    save("toy_pavrm", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl"]
+    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl", "pavrm"]
+    if "pavrm" in which:
+        case_toy_pavrm()
     if "ops" in which:
         case_ops()
     if "toy" in which:

@@ -107,15 +107,57 @@ def test_real_width_block_vs_reference(golden, tag):
     assert abs(dmod.double().norm().item() / float(g["gnorm/modulation"]) - 1) < 3e-2
 
 
-def test_attention_stash_is_bit_identical():
+def test_real_width_block_long_L_vs_oracle():
+    """14B block (C = 5120, 40 heads, F = 13 824) at L = 4 200 (3 x 35 x 40 tokens: L >= 4096
+    selects the production self-attention kernels, L % 96 = 72, L % 256 = 104), with the
+    attention-output stash on (the backward reuses the forward's kept (ao, lse)), vs the CPU
+    oracle: output, input / modulation / context gradients and every parameter gradient."""
+    from prfl_amd import block as B
+    torch.set_num_threads(16)
+    P = seeded_params(block_shapes("blocks.0.", 5120, 13824, False), prefix="long.")
+    grid = (3, 35, 40)
+    L, Lc = 4200, 512
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(1, L, 5120, generator=g)
+    e = torch.randn(1, 6, 5120, generator=g) * 0.1
+    ctx = torch.randn(1, Lc, 5120, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, 5120, generator=g)
+    try:
+        B.set_attn_stash_budget(1 << 30)
+        out, dx, de, dmod, dctx, G = run_block(P, x, e, ctx, grid, L, 40, False, up)
+    finally:
+        B.set_attn_stash_budget(0)
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    xr, er = x.clone().requires_grad_(True), e.clone().requires_grad_(True)
+    cr = ctx.float().requires_grad_(True)
+    ref = O.block_forward(Pr, "blocks.0.", xr, er, torch.tensor([grid]), O.rope_freqs(128), cr,
+                          40, seq_len=L)
+    (ref * up).sum().backward()
+    assert rel(out, ref) < 1e-2, rel(out, ref)
+    assert rel(dx, xr.grad) < 3e-2, rel(dx, xr.grad)
+    assert rel(de, er.grad) < 3e-2, rel(de, er.grad)
+    assert rel(dmod, Pr["blocks.0.modulation"].grad) < 3e-2
+    assert rel(dctx.float(), cr.grad) < 3e-2
+    grads = {"grad/" + k: v.grad.numpy() for k, v in Pr.items() if v.grad is not None}
+    for n, gr in G.items():
+        refg = Pr["blocks.0." + n].grad
+        scale = key_path_scale(grads, "blocks.0." + n)
+        if scale is not None:
+            assert (gr.cpu() - refg).norm() < 3e-2 * scale, n
+        else:
+            assert rel(gr, refg) < 3e-2, (n, rel(gr, refg))
+
+
+@pytest.mark.parametrize("L,grid", [(105, (3, 5, 7)), (4200, (3, 35, 40))])
+def test_attention_stash_is_bit_identical(L, grid):
     """Keeping the self-attention output/LSE for the backward (block.set_attn_stash_budget)
-    gives bit-identical outputs and gradients to the plain checkpoint recompute."""
+    gives bit-identical outputs and gradients to the plain checkpoint recompute (L = 4 200 runs
+    the production long-KV attention kernels)."""
     from prfl_amd import block as B
     from prfl_amd import ops
     dim, ffn, nh = 256, 512, 2
     P = seeded_params(block_shapes("blocks.0.", dim, ffn, False), prefix="stash.")
     g = torch.Generator().manual_seed(3)
-    L, grid = 105, (3, 5, 7)
     x = torch.randn(1, L, dim, generator=g)
     e = torch.randn(1, 6, dim, generator=g) * 0.1 + P["blocks.0.modulation"]
     ctx = torch.randn(1, 512, dim, generator=g).to(torch.bfloat16)

@@ -57,6 +57,89 @@ def test_gemm_forward_epilogues(ops, M, N, K):
     assert torch.equal(o, res + y.float() * gate)
 
 
+def _tile_diff(a, b, tile=256):
+    """[(tile_m, tile_n, quadrant, n_bad)] of the output elements where a != b."""
+    bad = (a != b)
+    if bad.dim() == 1:
+        bad = bad[None]
+    idx = bad.nonzero()
+    out = {}
+    for m, n in idx[:4096].tolist():
+        key = (m // tile, n // tile, (m % tile) // (tile // 2), (n % tile) // (tile // 2))
+        out[key] = out.get(key, 0) + 1
+    return sorted(out.items())[:16]
+
+
+# (M, N, K): the round-1 failing shape, then the 720p x 81f block projections (L = 73 920):
+# fused QKV, o-proj / FFN-down with the gated residual, FFN-up with GELU
+_CROSS_SHAPES = [(4096, 5120, 1024), (73920, 15360, 5120), (73920, 5120, 5120),
+                 (73920, 13824, 5120), (73920, 5120, 13824)]
+
+
+@pytest.mark.parametrize("M,N,K", _CROSS_SHAPES)
+def test_gemm_tiles_bit_identical_forward(ops, M, N, K):
+    """The 256x256 staggered-ring kernel and the 128x128 kernel sum every element in the same
+    k order (t, then the two 32-deep k-steps), so every epilogue must agree bit for bit.  A
+    mismatch names the 256-tiles / quadrants that differ; comparing y = aux with the residual
+    output separates an accumulator (ring / barrier) fault from an epilogue fault."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    bias = (torch.randn(N, generator=g, device=DEV) * 0.1).to(torch.bfloat16)
+    res = torch.randn(M, N, generator=g, device=DEV)
+    gate = torch.randn(N, generator=g, device=DEV) * 0.5
+    outs = {}
+    for tile in (128, 256):
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        o = ops.linear(a, w, bias, ops.EPI_RESID, gate=gate, res=res, aux=y, tile=tile)
+        assert torch.equal(o, res + y.float() * gate), f"tile {tile}: residual epilogue"
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        act = ops.linear(a, w, bias, ops.EPI_GELU, aux=pre, tile=tile)
+        outs[tile] = dict(bf16=ops.linear(a, w, bias, tile=tile), y=y, o=o, pre=pre, act=act,
+                          f32=ops.linear(a, w, None, ops.EPI_F32, tile=tile))
+        torch.cuda.synchronize()
+    for key in outs[128]:
+        x128, x256 = outs[128][key], outs[256][key]
+        assert torch.equal(x128, x256), (key, _tile_diff(x128, x256))
+    # residual output aliasing its input (the block's in-place x += o-proj * gate)
+    xr = res.clone()
+    ops.linear(a, w, bias, ops.EPI_RESID, out=xr, gate=gate, res=xr)
+    assert torch.equal(xr, outs[256]["o"])
+    # and one check against an independent fp32 GEMM of the same bf16 operands
+    rows = torch.arange(0, M, max(1, M // 257), device=DEV)
+    ref = a[rows].float() @ w.float().t()
+    assert rel(outs[256]["f32"][rows], ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(5120, 13824, 73920), (5120, 5120, 32760), (13824, 5120, 4096)])
+def test_gemm_tiles_bit_identical_weight_grad(ops, M, N, K):
+    """dW = dY^T X (both operands MN-major, ds_read_b64_tr_b16 path) and dX = dY W: 256 vs 128
+    tile.  K = 32760 (480p tokens, K % 64 = 56) takes the bulk + tail split on the 256 path, so
+    there only the fp32 reference check applies."""
+    g = torch.Generator(device=DEV).manual_seed(M * 3 + N)
+    dy = torch.randn(K, M, generator=g, device=DEV).to(torch.bfloat16)
+    x = torch.randn(K, N, generator=g, device=DEV).to(torch.bfloat16)
+    dws = [ops.linear_dw(dy, x, out=torch.empty(M, N, device=DEV)) for _ in range(1)]
+    ref_rows = torch.arange(0, M, 97, device=DEV)
+    ref = dy[:, ref_rows].float().t() @ x.float()
+    assert rel(dws[0][ref_rows], ref) < 1e-5
+    if K % 64 == 0:
+        d128 = torch.empty(M, N, device=DEV)
+        ops.gemm(dy, x, d128, M, N, K, False, False, ops.EPI_F32, tile=128)
+        d256 = torch.empty(M, N, device=DEV)
+        ops.gemm(dy, x, d256, M, N, K, False, False, ops.EPI_F32, tile=256)
+        assert torch.equal(d128, d256), _tile_diff(d128, d256)
+        assert torch.equal(d256, dws[0])
+    # dX[K, N] = dY[K, M] @ W[M, N]: B MN-major
+    w = (torch.randn(M, N, generator=g, device=DEV) / math.sqrt(M)).to(torch.bfloat16)
+    outs = []
+    for tile in (128, 256):
+        dx = torch.empty(K, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(dy, w, dx, K, N, M, True, False, ops.EPI_BF16, tile=tile)
+        outs.append(dx)
+    assert torch.equal(outs[0], outs[1]), _tile_diff(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 384, 128), (105, 256, 296), (1000, 136, 520),
                                    (3072, 2048, 3072), (3000, 2048, 3072)])
 def test_gemm_backward_layouts(ops, M, N, K):
@@ -109,6 +192,108 @@ def test_attention_fwd_bwd(ops, Lq, Lk, H, klen):
     assert rel(dv, vr.grad.reshape(Lk, C)) < 2e-2
     if klen < Lk:
         assert dk[klen:].abs().max().item() == 0 and dv[klen:].abs().max().item() == 0
+
+
+def _lse2_ref(q, k, H, klen, scale):
+    """log2-domain row LSE of softmax(q k^T * scale) over keys < klen; q/k bf16 [L, H*128]."""
+    Lq, Lk = q.shape[0], k.shape[0]
+    qh = q.float().view(Lq, H, 128).transpose(0, 1)
+    kh = k.float().view(Lk, H, 128).transpose(0, 1)
+    s = torch.bmm(qh, kh.transpose(1, 2))[:, :, :klen] * scale
+    return torch.logsumexp(s, -1) / math.log(2.0)
+
+
+@pytest.mark.parametrize("Lq,Lk,H,klen", [(4200, 4200, 2, 4133), (4133, 4133, 1, 4133),
+                                          (1000, 4100, 2, 4097), (4111, 5000, 1, 4500)])
+def test_attention_long_kv_vs_oracle(ops, Lq, Lk, H, klen):
+    """The production self-attention instantiation (Lk >= 4096 -> attn_fwd_kernel<false, 2, 3>,
+    the L x L forward of every block) and both backward kernels vs the CPU oracle: L not a
+    multiple of 96 or 256 (the clamped last K/V tile, partial query tiles), k_len < Lk."""
+    g = torch.Generator().manual_seed(Lq * 3 + Lk)
+    C = H * 128
+    q = bf(torch.randn(Lq, C, generator=g) * 1.5)
+    k = bf(torch.randn(Lk, C, generator=g) * 1.5)
+    v = bf(torch.randn(Lk, C, generator=g))
+    o, lse = ops.attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), H, k_len=klen)
+    qr = q.float().view(1, Lq, H, 128).requires_grad_(True)
+    kr = k.float().view(1, Lk, H, 128).requires_grad_(True)
+    vr = v.float().view(1, Lk, H, 128).requires_grad_(True)
+    ref = O.attention(qr, kr, vr, k_len=klen if klen < Lk else None)
+    assert rel(o, ref.reshape(Lq, C)) < 5e-3
+    lref = _lse2_ref(q, k, H, klen, 1 / math.sqrt(128))
+    assert (lse.cpu() - lref).abs().max().item() < 1e-3
+    do = bf(torch.randn(Lq, C, generator=g))
+    ref.backward(do.float().view(1, Lq, H, 128))
+    dq, dk, dv = ops.attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), o, do.to(DEV), lse, H, k_len=klen)
+    assert rel(dq, qr.grad.reshape(Lq, C)) < 2e-2
+    assert rel(dk, kr.grad.reshape(Lk, C)) < 2e-2
+    assert rel(dv, vr.grad.reshape(Lk, C)) < 2e-2
+    if klen < Lk:
+        assert dk[klen:].abs().max().item() == 0 and dv[klen:].abs().max().item() == 0
+
+
+def _attention_ref_gpu(q, k, v, do, H, scale, chunk=4096):
+    """fp32 FA2-numerics reference (oracle/_FlashAttention restated in query chunks on the GPU
+    for full-size L): P rounded to bf16 for P.V, the normaliser sums fp32 P, bf16 output,
+    D = rowsum(dO * bf16 O)."""
+    L, C = q.shape
+    Lk = k.shape[0]
+    o = torch.empty(L, C, dtype=torch.bfloat16, device=DEV)
+    lse2 = torch.empty(H, L, device=DEV)
+    dq = torch.empty(L, C, device=DEV)
+    dk = torch.zeros(Lk, C, device=DEV)
+    dv = torch.zeros(Lk, C, device=DEV)
+    for h in range(H):
+        sl = slice(h * 128, (h + 1) * 128)
+        kh, vh = k[:, sl].float(), v[:, sl].float()
+        for c0 in range(0, L, chunk):
+            cs = slice(c0, min(L, c0 + chunk))
+            qh, doh = q[cs, sl].float(), do[cs, sl].float()
+            s = (qh @ kh.t()) * scale
+            m = s.amax(-1, keepdim=True)
+            p = torch.exp(s - m)
+            l = p.sum(-1, keepdim=True)
+            oh = ((p.to(torch.bfloat16).float() @ vh) / l).to(torch.bfloat16)
+            o[cs, sl] = oh
+            lse2[h, cs] = ((m + torch.log(l)) / math.log(2.0)).squeeze(-1)
+            P = p / l
+            del p, s
+            dv[:, sl] += P.t() @ doh
+            dp = doh @ vh.t()
+            delta = (doh * oh.float()).sum(-1, keepdim=True)
+            ds = P * (dp - delta)
+            del P, dp
+            dq[cs, sl] = (ds @ kh) * scale
+            dk[:, sl] += (ds.t() @ qh) * scale
+            del ds
+    return o, lse2, dq, dk, dv
+
+
+@pytest.mark.parametrize("L,H", [(32760, 2), (73920, 1)])
+def test_attention_full_size_vs_reference(ops, L, H):
+    """Self-attention at the real token counts (480p x 81f: L = 32 760, L % 96 = 24, L % 256 =
+    248; 720p x 81f: L = 73 920) against an fp32 GPU restatement of the FA2 numerics; the
+    forward rows are also checked against an fp64 CPU computation over all keys."""
+    g = torch.Generator(device=DEV).manual_seed(L)
+    C = H * 128
+    q = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
+    k = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
+    v = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
+    do = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
+    scale = 1 / math.sqrt(128)
+    o, lse = ops.attn_fwd(q, k, v, H)
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, H)
+    ro, rlse, rdq, rdk, rdv = _attention_ref_gpu(q, k, v, do, H, scale)
+    assert rel(o, ro) < 5e-3
+    assert (lse - rlse).abs().max().item() < 1e-3
+    assert rel(dq, rdq) < 2e-2 and rel(dk, rdk) < 2e-2 and rel(dv, rdv) < 2e-2
+    rows = torch.randperm(L, generator=torch.Generator().manual_seed(1))[:64].sort().values
+    qc = q[rows.to(DEV)].double().cpu().view(64, H, 128).transpose(0, 1)
+    kc = k.double().cpu().view(L, H, 128).transpose(0, 1)
+    vc = v.double().cpu().view(L, H, 128).transpose(0, 1)
+    p = torch.softmax(torch.bmm(qc, kc.transpose(1, 2)) * scale, -1)
+    exact = torch.bmm(p, vc).transpose(0, 1).reshape(64, C)
+    assert rel(o[rows.to(DEV)], exact) < 5e-3
 
 
 def test_attention_rescale_spike(ops):

@@ -5,7 +5,7 @@
 out=$GRAFT_REPO_ROOT/gpurun_out/${1:-pmcbench}; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
-  --kernel-include-regex attn_fwd_pp3 -d $out/prof -o bench --output-format csv \
+  --kernel-include-regex attn_fwd_kernel -d $out/prof -o bench --output-format csv \
   -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --warmup 0 --steps 1 > $out/bench.json 2> $out/bench.err
 rc=$?
 cat $out/bench.json; ls -R $out/prof | head
