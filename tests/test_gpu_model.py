@@ -185,3 +185,95 @@ def test_flash_attention_api():
     for b, kl in enumerate([90, 41]):
         ref = O.attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], k_len=kl if kl < 90 else None)
         assert rel(out[b:b + 1], ref) < 5e-3
+
+
+def test_toy_pavrm_steps_vs_reference(golden):
+    """Two PAVRM 'ce' steps (train_pavrm.py:671-920) through PAVRMTrainer vs the reference run
+    of make_golden.case_toy_pavrm: features, probability, BCE loss, every trunk / QueryAttention /
+    MLP gradient and the transformer grad norm (clip_grad_norm_ over the trunk only) of both
+    steps (the second on AdamW-updated weights).  The update itself is checked against
+    torch.optim.AdamW with the reference's three parameter groups, given our clipped grads."""
+    from prfl_amd.network import MLP, QueryAttention
+    from prfl_amd.train import PAVRMTrainer
+    g = golden("toy_pavrm")
+    lrm = toy_model("t2v")
+    lrm.blocks = torch.nn.ModuleList(list(lrm.blocks))
+    del lrm.head
+    lrm.head = None
+    qa = QueryAttention(256, 1, 8, 0., return_type="query")
+    qa.load_state_dict(seeded_params(qa_shapes(256), prefix="pqa."))
+    mlp = MLP(256)
+    mlp.load_state_dict(seeded_params(mlp_shapes(256), prefix="pmlp."))
+    qa, mlp = qa.to(DEV), mlp.to(DEV)
+    tr = PAVRMTrainer(lrm, qa, mlp, feature_layer=(2,))
+    assert tr.opt_trunk.lr == tr.opt_head.lr == 1e-6          # learning_rate_mlp unset (CE)
+    named = {**dict(lrm.named_parameters()), **{"qa." + k: v for k, v in qa.named_parameters()},
+             **{"mlp." + k: v for k, v in mlp.named_parameters()}}
+    ctx = torch.from_numpy(g["ctx"]).to(DEV).to(torch.bfloat16)
+    grads = {}
+    orig_step = {}
+
+    def capture(opt, tag):          # grads as the optimizer sees them (after the trunk clip)
+        f = opt.step
+
+        def step():
+            grads[tag] = [p.grad.detach().clone() for p in opt.params]
+            orig_step[tag] = [p.detach().clone() for p in opt.params]
+            f()
+        opt.step = step
+    capture(tr.opt_trunk, "trunk")
+    capture(tr.opt_head, "head")
+    ref_states = {}
+    for s in range(2):
+        x0 = torch.from_numpy(g[f"s{s}:x0"]).to(DEV).to(torch.bfloat16)
+        noise = torch.from_numpy(g[f"s{s}:noise"]).to(DEV).to(torch.bfloat16)
+        t = tr.fm.timesteps[[int(g[f"s{s}:idx"])]].to(DEV)
+        label = torch.tensor([float(g[f"s{s}:label"])], device=DEV)
+        # raw (pre-clip) grads: record them in a backward hook of the reducer's end()
+        raw = {}
+        end = tr.reducer.end
+
+        def end_hook():
+            end()
+            for n, p in named.items():
+                if p.grad is not None:
+                    raw[n] = p.grad.detach().clone()
+        tr.reducer.end = end_hook
+        out = tr.step(x0, ctx, 105, label, noise=noise, timestep=t)
+        tr.reducer.end = end
+        assert abs(float(out["prob"].flatten()[0]) - float(g[f"s{s}:prob"].flatten()[0])) < 3e-3
+        assert abs(float(out["loss"]) / float(g[f"s{s}:loss"]) - 1) < 1e-2
+        assert abs(float(out["grad_norm"]) / float(g[f"s{s}:grad_norm"]) - 1) < 3e-2
+        n_checked = 0
+        for k, v in g.items():
+            if not k.startswith(f"s{s}:"):
+                continue
+            key = k[len(f"s{s}:"):]
+            for kind in ("grad/", "gnorm/"):
+                if kind in key:
+                    pre, n = key.split(kind)
+                    n = pre + n
+                    got = raw[n]
+                    if kind == "grad/":
+                        scale = key_path_scale({"grad/" + kk.split("grad/")[1]: vv for kk, vv in g.items()
+                                                if kk.startswith(f"s{s}:{pre}grad/")}, n[len(pre):])
+                        if scale is not None:
+                            assert (got.cpu().flatten() - torch.from_numpy(v)).norm().item() < 3e-2 * scale, n
+                        else:
+                            assert rel(got, v) < 3e-2, (s, n, rel(got, v))
+                    else:
+                        assert abs(got.double().norm().item() / float(v) - 1) < 3e-2, (s, n)
+                    n_checked += 1
+        assert n_checked > 30
+        # the update: torch.optim.AdamW (reference groups) on the same clipped grads
+        for tag, opt in (("trunk", tr.opt_trunk), ("head", tr.opt_head)):
+            ps = [p.clone().requires_grad_(True) for p in orig_step[tag]]
+            ref = torch.optim.AdamW(ps, lr=1e-6, betas=(0.9, 0.999), weight_decay=0.01, eps=1e-8)
+            if s == 1:
+                ref.load_state_dict(ref_states[tag])
+            for p, gr in zip(ps, grads[tag]):
+                p.grad = gr
+            ref.step()
+            for p, q in zip(ps, opt.params):
+                assert (p.detach() - q.detach()).abs().max().item() <= 1e-9 + 1e-6 * p.abs().max().item()
+            ref_states[tag] = ref.state_dict()
