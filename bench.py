@@ -204,17 +204,17 @@ def main():
     if args.fp8:
         gen.set_fp8_gemm(True)
         lrm.set_fp8_gemm(True)
-    # keep the self-attention outputs of the first blocks of every grad-enabled model forward
-    # for the backward (bit-identical to recomputing them).  T2V: 32 GB keeps all 40 blocks at
-    # 720p (0.76 GB each), so no grad-enabled L x L attention forward is recomputed: peak 247 GB
-    # allocated / 290 GB reserved of the 309 GB (288 GiB) card at N = 1, 143.98 s/iter vs 147.8 s
-    # at 12 GB and 153.2 s without (profiles/r01_bench_prfl720_notes.txt); 20 GB (peak 281 GB
-    # reserved) when RCCL's buffers sit beside it (N > 1).  I2V (16.4 B parameters): 16 GB at
-    # N = 1 (peak 254 allocated / 302 reserved; 32 GB runs out of memory), none at N > 1.
+    # keep the self-attention outputs of the first blocks of every graph-recording model forward
+    # for the backward (bit-identical to recomputing them); the budget is per training step and
+    # shared by the generator's and the reward model's forwards (block.py).  T2V: 38 GB keeps
+    # all 40 generator blocks + the 8 reward-model blocks at 720p (0.77 GB each), so no
+    # grad-enabled L x L attention forward is recomputed (round 1: 32 GB per model forward, peak
+    # 247 GB allocated / 290 GB reserved of the 309 GB card); 20 GB when RCCL's buffers sit
+    # beside it (N > 1).  I2V (16.4 B parameters): 22 GB at N = 1, none at N > 1.
     from prfl_amd import block as _blk
     default_gb = "0"
     if big_fits(args):
-        default_gb = ("16" if world == 1 else "0") if i2v else ("32" if world == 1 else "20")
+        default_gb = ("22" if world == 1 else "0") if i2v else ("38" if world == 1 else "20")
     stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB", default_gb))
     _blk.set_attn_stash_budget(int(stash_gb * 1e9))
     g = torch.Generator(device=dev).manual_seed(110221 + rank)   # distinct data per rank

@@ -133,6 +133,6 @@ void set_work(double w);  // algorithmic FLOPs/bytes of the launch being timed
 }
 enum {
   KID_GEMM = 0, KID_ATTN_FWD, KID_ATTN_FWD_SHORT, KID_ATTN_BWD_DKDV, KID_ATTN_BWD_DQ, KID_LN, KID_RMS,
-  KID_ELTWISE, KID_ADAMW,
+  KID_ELTWISE, KID_ADAMW, KID_POOL,
   KID_COUNT
 };

@@ -1,0 +1,3 @@
+# import path of the reference (diffusers_lite/utils/fsdp_utils.py); implementation: prfl_amd.fsdp_utils
+from prfl_amd.fsdp_utils import (apply_fsdp_checkpointing, get_dit_fsdp_kwargs,  # noqa: F401
+                                 get_mixed_precision, non_reentrant_wrapper)

@@ -43,14 +43,18 @@ SIGNATURES = {
                       P],
     "prfl_unipc_step": [P, P, P, P, P, P, P, P, I64, P, I32, I32, P],
     "prfl_unipc_step_bwd": [P, P, I64, P, I32, I32, P],
+    "prfl_query_pool_splits": [I64, I64, I64],
+    "prfl_query_pool_fwd": [P, I64, P, I64, I64, I64, I64, I64, I64, F32, P, I64, P, P, P, P, I64, P],
+    "prfl_query_pool_bwd": [P, P, I64, P, I64, I64, P, P, I64, I64, I64, I64, F32, P, I64, P, I64,
+                            I64, P, I64, P],
     "prfl_prof_enable": [I32],
     "prfl_prof_collect": [P, P, P, I32],
 }
 
 # kernel ids of the profiling hooks (csrc/common.h)
 KID = dict(gemm=0, attn_fwd=1, attn_fwd_short=2, attn_bwd_dkdv=3, attn_bwd_dq=4, ln=5, rms=6,
-           eltwise=7, adamw=8)
-NKID = 9
+           eltwise=7, adamw=8, pool=9)
+NKID = 10
 
 _lib = None
 

@@ -1,6 +1,7 @@
 """Fused WanAttentionBlock forward/backward on the HIP kernels (`model.py:280-359`).
 
-The block is one autograd node (``WanBlockFn``) that implements the reference's non-reentrant
+The block is one autograd node (the ``prfl::wan_block`` custom op, custom_ops.py) that implements
+the reference's non-reentrant
 activation checkpoint (`fsdp_utils.py:17-50`, every block checkpointed): the forward keeps only the
 block input; the backward re-runs the forward saving what the backward kernels need, then runs
 the hand-written backward chain.  fp32 master weights are cast to bf16 once per pass into
@@ -35,10 +36,13 @@ def param_names(i2v):
 
 
 # Attention-output stash (memory-for-time trade on top of the reference's per-block checkpoint):
-# a block whose forward runs with grad may keep its self-attention output and LSE (L*C*2 + H*L*4
-# bytes per sample) so the backward's recompute skips the L x L attention forward — the kernels
-# are deterministic, so the recomputed and the kept tensors are bit-identical.  The budget is per
-# model forward (WanModel.forward resets it); 0 (the default) keeps the pure checkpoint.
+# a block whose forward records a graph may keep its self-attention output and LSE (L*C*2 +
+# H*L*4 bytes per sample) so the backward's recompute skips the L x L attention forward — the
+# kernels are deterministic, so the recomputed and the kept tensors are bit-identical.  The budget
+# is per training step: the trainer calls reset_attn_stash() at the start of every SFT / reward /
+# PAVRM step, so the generator's and the reward model's forwards of one step share it and the
+# stash never exceeds the budget.  0 (the default) keeps the pure checkpoint.  Under an external
+# torch.utils.checkpoint leave it at 0: that recompute would see a different keep decision.
 _STASH = {"budget": 0, "left": 0}
 
 
@@ -310,58 +314,25 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     return dx, torch.stack(de), dctx
 
 
-class WanBlockFn(torch.autograd.Function):
-    """Checkpointed fused block: forward(x [B,L,C], e [B,6,C], ctx [B,Lc,C] bf16, *params)."""
-
-    @staticmethod
-    def forward(fctx, x, e, context, meta, names, *params):
-        P = dict(zip(names, params))
-        W = BF16Weights(P, fp8=meta.fp8, need_bf16=False)
-        L, C = x.shape[1], x.shape[2]
-        need = x.shape[0] * (L * C * 2 + meta.num_heads * L * 4)
-        keep = any(fctx.needs_input_grad) and _STASH["left"] >= need
-        if keep:
-            _STASH["left"] -= need
-        outs, kept = [], []
-        for b in range(x.shape[0]):
-            o, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False,
-                                     keep_attn=keep)
-            outs.append(o)
-            if keep:
-                kept.append(S["attn"])
-        del W
-        fctx.attn = kept if keep else None
-        fctx.meta, fctx.names = meta, names
-        fctx.save_for_backward(x, e, context, *params)
-        return outs[0].unsqueeze(0) if len(outs) == 1 else torch.stack(outs)
-
-    @staticmethod
-    def backward(fctx, dout):
-        x, e, context, *params = fctx.saved_tensors
-        meta, names = fctx.meta, fctx.names
-        P = dict(zip(names, params))
-        W = BF16Weights(P, fp8=meta.fp8)
-        G = {}
-        dxs, des, dcs = [], [], []
-        kept, fctx.attn = fctx.attn, None
-        for b in range(x.shape[0]):
-            _, S = block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=True,
-                                     attn=kept[b] if kept else None)
-            d = dout[b].to(torch.float32).contiguous().clone()
-            dx, de, dc = block_backward_one(P, W, x[b], e[b], context[b], meta, b, S, d, G,
-                                            want_w=any(fctx.needs_input_grad[5:]))
-            del S
-            dxs.append(dx)
-            des.append(de)
-            dcs.append(dc)
-        dx = (dxs[0].unsqueeze(0) if len(dxs) == 1 else torch.stack(dxs)).to(x.dtype)
-        de = torch.stack(des)
-        dctx = torch.stack(dcs).to(context.dtype) if context.requires_grad else None
-        pg = [G.get(n) if p.requires_grad else None for n, p in zip(names, params)]
-        return (dx, de, dctx, None, None, *pg)
-
-
 def block_apply(P, x, e, context, meta):
-    """P: ordered dict name -> fp32 parameter (the block's, without 'modulation')."""
-    names = tuple(P.keys())
-    return WanBlockFn.apply(x, e, context, meta, names, *P.values())
+    """The fused, checkpointed block through the `prfl::wan_block` custom op (its backward is
+    `prfl::wan_block_backward`).  P: name -> fp32 parameter (the block's, without
+    'modulation'); x [B, L, C], e [B, 6, C] fp32 (modulation + e0), context [B, Lc, C] bf16.
+
+    The self-attention output / LSE is kept for the backward only when this forward records a
+    graph (grad mode on and some input requires grad) and the per-step stash budget has room."""
+    from . import custom_ops
+    params = [P[n] for n in param_names(meta.i2v)]
+    L, C = x.shape[1], x.shape[2]
+    need = x.shape[0] * (L * C * 2 + meta.num_heads * L * 4)
+    records = torch.is_grad_enabled() and (x.requires_grad or e.requires_grad or
+                                           context.requires_grad or
+                                           any(p.requires_grad for p in params))
+    keep = records and _STASH["left"] >= need
+    if keep:
+        _STASH["left"] -= need
+    grid = [int(v) for g in meta.grid for v in g]
+    out, _, _ = custom_ops.wan_block(x, e, context, params, int(meta.num_heads), grid,
+                                     [int(v) for v in meta.seq_len], meta.rope_tab, bool(meta.i2v),
+                                     float(meta.eps), bool(meta.fp8), keep)
+    return out

@@ -5,8 +5,9 @@ and identical forward signatures, so scripts/prfl and scripts/pavrm drive it as 
 reference.
 
 What runs where:
-  * every WanAttentionBlock  -> one fused, checkpointed HIP autograd node (prfl_amd/block.py)
-  * patch / text / image embeddings (bf16 Linear under autocast) -> HIP GEMM (prfl_amd/linear.py)
+  * every WanAttentionBlock  -> the fused, checkpointed `prfl::wan_block` custom op
+    (prfl_amd/custom_ops.py, prfl_amd/block.py)
+  * patch / text / image embeddings (bf16 Linear under autocast) -> `prfl::linear_bf16`
   * fp32 islands the reference keeps in fp32 (time embedding MLP on [B, 256]; Head's
     LayerNorm + 5120->64 Linear; unpatchify) -> small fp32 torch ops on the GPU (< 0.1 % of the
     step's FLOPs).
@@ -141,6 +142,7 @@ class WanAttentionBlock(nn.Module):
     """model.py:280-359.  forward() is one fused, activation-checkpointed HIP autograd node."""
 
     fp8_gemm = False    # config C5's fp8 path (WanModel.set_fp8_gemm); the reference is bf16-only
+    self_checkpointing = True   # forward is already the per-block checkpoint (fsdp_utils.py)
 
     def __init__(self, cross_attn_type, dim, ffn_dim, num_heads, window_size=(-1, -1),
                  qk_norm=True, cross_attn_norm=False, eps=1e-6):
@@ -161,13 +163,21 @@ class WanAttentionBlock(nn.Module):
         self.modulation = nn.Parameter(torch.randn(1, 6, dim) / dim ** 0.5)
         self._names = B.param_names(self.i2v)
 
+    def _param(self, name):
+        """Parameter by attribute path, not named_parameters(): under FSDP (use_orig_params
+        False, as `train_prfl.py:361` wraps it) the block's parameters are plain tensor views
+        of the all-gathered flat parameter during forward / backward."""
+        obj = self
+        for part in name.split("."):
+            obj = getattr(obj, part)
+        return obj
+
     def forward(self, x, e, seq_lens, grid_sizes, freqs, context, context_lens):
         assert e.dtype == torch.float32
         assert context_lens is None, "cross-attention keys are unmasked in the reference (model.py:597)"
         with torch.autocast("cuda", enabled=False):
             em = self.modulation + e                                   # model.py:340
-            params = dict(self.named_parameters())
-            P = {n: params[n] for n in self._names}
+            P = {n: self._param(n) for n in self._names}
             meta = B.Meta(self.num_heads, [tuple(g) for g in grid_sizes.tolist()],
                           [int(s) for s in seq_lens.tolist()], _rope_table(freqs, x.device),
                           self.i2v, self.eps, fp8=self.fp8_gemm)
@@ -277,9 +287,11 @@ class WanModel(nn.Module):
         return cls(**{k: v for k, v in cfg.items() if k in keep})
 
     @classmethod
-    def from_pretrained(cls, path, **kw):
+    def from_pretrained(cls, path, allow_missing=(), **kw):
         """Loads a diffusers-format directory: config.json + *.safetensors (sharded or not),
-        as written by `utils/model_utils.py:70-125` and the Wan2.1 releases."""
+        as written by `utils/model_utils.py:70-125` and the Wan2.1 releases.  A checkpoint that
+        leaves parameters unset (wrong model type, truncated shard) raises instead of silently
+        keeping their random init; `allow_missing` lists key prefixes that may be absent."""
         from safetensors.torch import load_file
         with open(os.path.join(path, "config.json")) as f:
             model = cls.from_config(json.load(f))
@@ -290,6 +302,10 @@ class WanModel(nn.Module):
         missing, unexpected = model.load_state_dict(sd, strict=False)
         if unexpected:
             raise RuntimeError(f"unexpected keys in checkpoint: {unexpected[:8]}")
+        missing = [k for k in missing if not any(k.startswith(a) for a in allow_missing)]
+        if missing:
+            raise RuntimeError(f"{len(missing)} parameters missing from checkpoint {path}: "
+                               f"{missing[:8]}")
         return model
 
     def save_pretrained(self, path, max_shard_bytes=5 * 1024 ** 3):
@@ -348,7 +364,6 @@ class WanModel(nn.Module):
                                                                  clip_fea, y)
         feats = []
         h = xb
-        B.reset_attn_stash()          # per-forward budget of kept attention outputs (block.py)
         for index, block in enumerate(self.blocks):
             h = block(h, e0, seq_lens, grid_sizes, self.freqs, ctx, None)
             if output_features and index + 1 in selected_layers:

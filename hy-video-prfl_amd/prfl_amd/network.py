@@ -3,14 +3,16 @@
 Same module tree and state-dict keys as the reference (an ``nn.MultiheadAttention`` is kept as the
 parameter container so `multihead_attn.in_proj_weight` etc. load unchanged).  The K/V
 in-projection over all L tokens (the only large product: [L,5120]x[5120,10240]) runs on the HIP
-GEMM; the single learned query's 8-head softmax pooling over L is a handful of [8, L] reductions.
-Precision = the reference under bf16 autocast: bf16 projections, fp32 softmax with P rounded to
-bf16 before P.V (flash / SDPA numerics), bf16 attention output.
+GEMM; the single learned query's 8-head softmax pooling over L is the split-L HIP kernel
+`prfl::query_pool` (csrc/pool.hip).  Precision = the reference under bf16 autocast: bf16
+projections, fp32 softmax with P rounded to bf16 before P.V (flash / SDPA numerics), bf16
+attention output.
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import custom_ops
 from .linear import linear_bf16
 
 BF16 = torch.bfloat16
@@ -33,23 +35,18 @@ class QueryAttention(nn.Module):
             nn.init.zeros_(self.text_proj.bias)
 
     def _pool(self, x, queries):
-        """x [N, L, E] (any float) -> attended [N, nq, E] bf16."""
+        """x [N, L, E] (any float) -> attended [N, nq, E] bf16.  The in-projections run on the
+        HIP GEMM (`prfl::linear_bf16`); the single-query softmax pooling over L is the
+        `prfl::query_pool` kernel (split over L, HBM-bound), one launch per query."""
         mha = self.multihead_attn
         E, H = self.feature_dim, self.num_heads
-        hd = E // H
         W, b = mha.in_proj_weight, mha.in_proj_bias
         N, L, _ = x.shape
         q = linear_bf16(queries, W[:E], b[:E])                       # [N, nq, E]
-        kv = linear_bf16(x.reshape(N * L, E), W[E:], b[E:]).view(N, L, 2, H, hd)
-        k, v = kv[:, :, 0], kv[:, :, 1]                              # [N, L, H, hd] bf16
-        with torch.autocast("cuda", enabled=False):
-            s = torch.einsum("nqhd,nlhd->nhql", q.view(N, -1, H, hd).float(), k.float())
-            s = s * hd ** -0.5
-            m = s.amax(-1, keepdim=True)
-            p = torch.exp(s - m)
-            l = p.sum(-1, keepdim=True)
-            o = torch.einsum("nhql,nlhd->nqhd", p.to(BF16).float(), v.float())
-            o = (o / l.permute(0, 2, 1, 3)).to(BF16).reshape(N, -1, E)
+        kv = linear_bf16(x.reshape(N * L, E), W[E:], b[E:]).view(N, L, 2 * E)
+        scale = float((E // H) ** -0.5)
+        o = torch.stack([custom_ops.query_pool(q[:, i].contiguous(), kv, H, scale)[0]
+                         for i in range(q.shape[1])], dim=1)         # [N, nq, E] bf16
         return linear_bf16(o, mha.out_proj.weight, mha.out_proj.bias)
 
     def forward(self, x, e=None, text=None):

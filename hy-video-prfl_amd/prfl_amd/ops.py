@@ -242,6 +242,47 @@ def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=No
     return dq, dk, dv
 
 
+def query_pool_fwd(q, kv, num_heads, scale, nsplit=None):
+    """Single-query attention pooling (csrc/pool.hip): q [N, E] bf16, kv [N, L, 2E] bf16 (k | v)
+    -> (o bf16 [N, E], lse2 fp32 [N, H])."""
+    _lib.require_gpu(q, kv)
+    assert q.dtype == BF16 and kv.dtype == BF16 and kv.stride(2) == 1
+    N, E = q.shape
+    L = kv.shape[1]
+    if nsplit is None:
+        nsplit = call_int_args("prfl_query_pool_splits", I64(N), I64(L), I64(num_heads))
+    hd = E // num_heads
+    o = torch.empty(N, E, dtype=BF16, device=q.device)
+    lse = torch.empty(N, num_heads, dtype=torch.float32, device=q.device)
+    pm = torch.empty(N * num_heads * nsplit, dtype=torch.float32, device=q.device)
+    pl = torch.empty_like(pm)
+    po = torch.empty(N * num_heads * nsplit * hd, dtype=torch.float32, device=q.device)
+    call("prfl_query_pool_fwd", ptr(q), I64(_ld(q)), ptr(kv), I64(kv.stride(1)), I64(kv.stride(0)),
+         I64(N), I64(L), I64(num_heads), I64(E), F32(scale), ptr(o), I64(E), ptr(lse), ptr(pm),
+         ptr(pl), ptr(po), I64(nsplit), stream_ptr())
+    return o, lse
+
+
+def query_pool_bwd(do, q, kv, o, lse, num_heads, scale, nsplit=None):
+    """-> (dq fp32 [N, E], dkv bf16 [N, L, 2E])."""
+    N, E = q.shape
+    L = kv.shape[1]
+    if nsplit is None:
+        nsplit = call_int_args("prfl_query_pool_splits", I64(N), I64(L), I64(num_heads))
+    hd = E // num_heads
+    dq = torch.empty(N, E, dtype=torch.float32, device=q.device)
+    dkv = torch.empty(N, L, 2 * E, dtype=BF16, device=q.device)
+    po = torch.empty(N * num_heads * nsplit * hd, dtype=torch.float32, device=q.device)
+    call("prfl_query_pool_bwd", ptr(do), ptr(q), I64(_ld(q)), ptr(kv), I64(kv.stride(1)),
+         I64(kv.stride(0)), ptr(o), ptr(lse), I64(N), I64(L), I64(num_heads), I64(E), F32(scale),
+         ptr(dq), I64(E), ptr(dkv), I64(2 * E), I64(L * 2 * E), ptr(po), I64(nsplit), stream_ptr())
+    return dq, dkv
+
+
+def call_int_args(name, *args):
+    return getattr(_lib.load(), name)(*args)
+
+
 def sumsq_(x, out):
     call("prfl_sumsq", ptr(x), I64(x.numel()), ptr(out), stream_ptr())
 
@@ -314,34 +355,3 @@ def unipc_step_bwd(grad_prev, coef, corr_order, pred_order):
     call("prfl_unipc_step_bwd", ptr(g), ptr(out), I64(g.numel()), ctypes.cast(cf, ctypes.c_void_p),
          I32(corr_order), I32(pred_order), stream_ptr())
     return out
-
-
-class UniPCStep(torch.autograd.Function):
-    """Differentiable w.r.t. model_output only — the one input that carries the reward
-    gradient at train_prfl.py:734 (the sample comes out of the no-grad rollout)."""
-
-    @staticmethod
-    def forward(ctx, model_output, sample, last_sample, hist1, hist2, coef, corr_order, pred_order):
-        ctx.coef, ctx.corr, ctx.pred = coef, corr_order, pred_order
-        ctx.set_materialize_grads(False)
-        m_t, sample_c, prev = unipc_step_fwd(sample, model_output, last_sample, hist1, hist2, coef,
-                                             corr_order, pred_order)
-        ctx.mark_non_differentiable(sample_c)
-        return m_t, sample_c, prev
-
-    @staticmethod
-    def backward(ctx, g_mt, g_sc, g_prev):
-        if g_mt is not None:
-            raise NotImplementedError("fused UniPC step: gradient through the stored m_t history")
-        gmo = None
-        if g_prev is not None:
-            gmo = unipc_step_bwd(g_prev, ctx.coef, ctx.corr, ctx.pred)
-        return gmo, None, None, None, None, None, None, None
-
-
-def unipc_step(model_output, sample, last_sample, hist1, hist2, coef, corr_order, pred_order):
-    for t in (sample, last_sample, hist1, hist2):
-        if t is not None and t.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("fused UniPC step differentiates w.r.t. model_output only")
-    return UniPCStep.apply(model_output, sample, last_sample, hist1, hist2, coef, corr_order,
-                           pred_order)

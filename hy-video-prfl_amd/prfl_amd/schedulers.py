@@ -4,7 +4,7 @@
   `train_prfl.py:413-415, :633` (`wan/utils/fm_solvers_unipc.py`, itself diffusers v0.31.0's UniPC
   adapted to flow matching).  The host computes the step's scalar coefficients exactly as the
   reference does (0-dim fp32 tensors, rhos cast to bf16); the element-wise body — model-output
-  conversion, UniC corrector and UniP predictor — is ONE fused HIP kernel (`ops.unipc_step`,
+  conversion, UniC corrector and UniP predictor — is ONE fused HIP kernel (`prfl::unipc_step`,
   csrc/unipc.hip), bit-identical to the reference's torch chain and differentiable w.r.t. the
   model output, through which the reward gradient flows (`train_prfl.py:734`).
 * FlowMatchDiscreteScheduler — training-time sigma/timestep sampling, add_noise, target
@@ -15,7 +15,7 @@ from types import SimpleNamespace
 import numpy as np
 import torch
 
-from . import ops
+from . import custom_ops
 
 
 class FlowUniPCMultistepScheduler:
@@ -117,7 +117,7 @@ class FlowUniPCMultistepScheduler:
         return [sig_t / sig_s0, alpha_t * h_phi_1, rk, alpha_t * B_h], self.this_order
 
     # the fused element-wise update (csrc/unipc.hip); tests swap in the oracle's restatement
-    _update = staticmethod(ops.unipc_step)
+    _update = staticmethod(custom_ops.unipc_update)
 
     def step(self, model_output, timestep, sample, return_dict=True, generator=None):
         if self.num_inference_steps is None:

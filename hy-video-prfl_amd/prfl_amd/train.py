@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import block as _block
 from .dist import GradReducer, all_reduce_mean, broadcast_int
 from .network import forward_mlp
 from .optim import AdamW, clip_grad_norm_
@@ -87,6 +88,7 @@ class PRFLTrainer:
     def sft_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
                  generator=None):
         """train_prfl.py:900-980."""
+        _block.reset_attn_stash()
         bsz = latents.shape[0]
         noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
                             device=latents.device)
@@ -104,6 +106,7 @@ class PRFLTrainer:
     def reward_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
                     mid_timestep=None, generator=None):
         """train_prfl.py:585-846."""
+        _block.reset_attn_stash()
         sch = self.unipc
         sch.set_timesteps(num_inference_steps=self.inference_steps, device=latents.device,
                           shift=self.flow_shift)
@@ -174,6 +177,7 @@ class PAVRMTrainer:
              generator=None, noise=None, timestep=None):
         """One PAVRM step; `noise` / `timestep` (values of the 1000-step schedule's `timesteps`,
         as `train_pavrm.py:721-728` passes them) replace the random draws when given."""
+        _block.reset_attn_stash()
         bsz = latents.shape[0]
         if noise is None:
             noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,

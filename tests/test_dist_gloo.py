@@ -9,6 +9,19 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+
+def _to_torch(obj):
+    """numpy payloads from the worker processes (sent by value: shared-memory tensor handles die
+    with a worker that has already exited) -> torch."""
+    import numpy as np
+    if isinstance(obj, np.ndarray):
+        return torch.from_numpy(obj)
+    if isinstance(obj, dict):
+        return {k: _to_torch(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_torch(v) for v in obj)
+    return obj
+
 def _worker(rank, world, port, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -25,7 +38,7 @@ def _worker(rank, world, port, out_q):
         red.end()
     mid = broadcast_int(17 if rank == 0 else 3)
     loss = all_reduce_mean(torch.tensor([float(rank)]))
-    out_q.put((rank, {n: p.grad.clone() for n, p in model.named_parameters()}, mid, loss.item()))
+    out_q.put((rank, {n: p.grad.numpy().copy() for n, p in model.named_parameters()}, mid, loss.item()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -37,7 +50,7 @@ def test_grad_reducer_gloo_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(2)]
+    res = [_to_torch(q.get(timeout=120)) for _ in range(2)]
     for p in procs:
         p.join(timeout=60)
     res.sort(key=lambda r: r[0])
@@ -80,7 +93,7 @@ def _zero1_worker(rank, world, port, out_q):
             p.grad = torch.randn(p.shape, generator=g)    # identical on both ranks (post all-reduce)
         opt.step()
     owned = sorted(i for i, p in enumerate(ps) if opt.owner[p] == rank)
-    out_q.put((rank, [p.detach().clone() for p in ps], owned, len(opt.state)))
+    out_q.put((rank, [p.detach().numpy().copy() for p in ps], owned, len(opt.state)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -93,7 +106,7 @@ def test_zero1_adamw_gloo_world2():
     procs = [ctx.Process(target=_zero1_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    res = sorted([_to_torch(q.get(timeout=120)) for _ in range(2)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
     (_, p0, own0, n0), (_, p1, own1, n1) = res
@@ -108,3 +121,65 @@ def test_zero1_adamw_gloo_world2():
             _adamw_ref(p, torch.randn(p.shape, generator=g), m, v, 1e-2, 0.9, 0.999, 1e-8, 0.01, step)
     for a, b, r in zip(p0, p1, ref):
         assert torch.equal(a, b) and torch.equal(a, r)
+
+
+class _DoneWork:
+    def wait(self):
+        return True
+
+
+def _avg_worker(rank, world, port, out_q):
+    """GradReducer's RCCL branch (ReduceOp.AVG, no host-side division) run over gloo: gloo has
+    no AVG, so AVG is emulated as SUM followed by the division RCCL performs internally."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from prfl_amd import dist as pdist
+    real = dist.all_reduce
+
+    def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
+        if op == dist.ReduceOp.AVG:
+            real(t, op=dist.ReduceOp.SUM)
+            t.div_(world)
+            return _DoneWork() if async_op else None
+        return real(t, op=op, async_op=async_op)
+    pdist.dist.all_reduce = all_reduce
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(300, 300), torch.nn.ReLU(), torch.nn.Linear(300, 7))
+    red = pdist.GradReducer(list(model.parameters()), small_numel=512)
+    red.backend = "nccl"                       # take the RCCL code path
+    assert red._op() == dist.ReduceOp.AVG
+    g = torch.Generator().manual_seed(100 + rank)
+    for micro in range(3):
+        x = torch.randn(4, 300, generator=g)
+        red.begin()
+        model(x).pow(2).mean().backward()
+        red.end()
+    pdist.dist.all_reduce = real
+    out_q.put((rank, {n: p.grad.numpy().copy() for n, p in model.named_parameters()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_rccl_branch_arithmetic_world2():
+    """The AVG path: after end() every rank holds acc + avg(fresh) without dividing again."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_avg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([_to_torch(q.get(timeout=120)) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, g0), (_, g1) = res
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(300, 300), torch.nn.ReLU(), torch.nn.Linear(300, 7))
+    gens = [torch.Generator().manual_seed(100 + r) for r in range(2)]
+    for micro in range(3):
+        for r in range(2):
+            x = torch.randn(4, 300, generator=gens[r])
+            (model(x).pow(2).mean() / 2).backward()
+    for n, p in model.named_parameters():
+        assert torch.allclose(g0[n], p.grad, atol=1e-6, rtol=1e-5), n
+        assert torch.equal(g0[n], g1[n]), n

@@ -13,6 +13,19 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(64, 33), (1000,), (7,), (300, 3), (5, 5), (128, 64)]
 
 
+
+def _to_torch(obj):
+    """numpy payloads from the worker processes (sent by value: shared-memory tensor handles die
+    with a worker that has already exited) -> torch."""
+    import numpy as np
+    if isinstance(obj, np.ndarray):
+        return torch.from_numpy(obj)
+    if isinstance(obj, dict):
+        return {k: _to_torch(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_torch(v) for v in obj)
+    return obj
+
 class _Toy(torch.nn.Module):
     def __init__(self):
         super().__init__()
@@ -53,7 +66,7 @@ def _worker(rank, world, port, out_q):
         opt.step()
         opt.zero_grad()
     opt.synchronize()
-    out_q.put((rank, [p.detach().cpu().clone() for p in model.parameters()], losses,
+    out_q.put((rank, [p.detach().cpu().numpy().copy() for p in model.parameters()], losses,
                sum(1 for p in opt.state)))
     dist.barrier()
     dist.destroy_process_group()
@@ -67,7 +80,7 @@ def test_zero1_streamed_overlapped_adamw_two_ranks_one_gpu():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=150) for _ in range(2)], key=lambda r: r[0])
+    res = sorted([_to_torch(q.get(timeout=150)) for _ in range(2)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
     (_, p0, l0, n0), (_, p1, l1, n1) = res
@@ -89,3 +102,82 @@ def test_zero1_streamed_overlapped_adamw_two_ranks_one_gpu():
     assert l0 == l1 == ref_losses
     for a, b, r in zip(p0, p1, model.parameters()):
         assert torch.equal(a, b) and torch.equal(a, r.detach().cpu())
+
+
+def _fused_worker(rank, world, port, out_q):
+    """Each rank: the toy WanModel (fused prfl::wan_block blocks) on its own sample, GradReducer
+    averaging the gradients across ranks during the backward, two accumulated micro-steps."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "hy-video-prfl_amd"), os.path.join(root, "tests", "golden")]
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from prfl_amd.dist import GradReducer
+    model = _toy_wan()
+    red = GradReducer([p for p in model.parameters() if p.requires_grad])
+    for micro in range(2):
+        x, ctx, up = _sample(rank, micro)
+        red.begin()
+        out = model(x=[x], t=torch.tensor([700], device="cuda"), context=[ctx], seq_len=105)[0]
+        (out * up).sum().backward()
+        red.end()
+    torch.cuda.synchronize()
+    out_q.put((rank, {n: p.grad.detach().cpu().numpy().copy() for n, p in model.named_parameters()
+                      if p.grad is not None}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _toy_wan():
+    from shapes import TOY, model_shapes, seeded_params
+    from prfl_amd.model import WanModel
+    m = WanModel(model_type="t2v", in_dim=16, **TOY)
+    m.load_state_dict(seeded_params(model_shapes(TOY, "t2v"), prefix="toy."))
+    return m.cuda()
+
+
+def _sample(rank, micro):
+    g = torch.Generator().manual_seed(1000 * rank + micro)
+    return (torch.randn(16, 3, 10, 14, generator=g).cuda(), torch.randn(20, 64, generator=g).cuda(),
+            torch.randn(16, 3, 10, 14, generator=g).cuda())
+
+
+def test_grad_reducer_fused_blocks_two_ranks_one_gpu():
+    """GradReducer with the fused block nodes (its post-accumulate-grad hooks fire as each fused
+    block's backward returns): every rank ends with sum_micro mean_rank(grad), bit-identical
+    across ranks and to the single-process reference that averages the per-rank gradients of
+    each micro-step in the same order (gloo SUM of two tensors, then / 2)."""
+    import sys
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_fused_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([_to_torch(q.get(timeout=200)) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, g0), (_, g1) = res
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    model = _toy_wan()
+    acc = {}
+    for micro in range(2):
+        per_rank = []
+        for r in range(2):
+            model.zero_grad(set_to_none=True)
+            x, ctx_, up = _sample(r, micro)
+            out = model(x=[x], t=torch.tensor([700], device="cuda"), context=[ctx_], seq_len=105)[0]
+            (out * up).sum().backward()
+            per_rank.append({n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()
+                             if p.grad is not None})
+        for n in per_rank[0]:
+            avg = (per_rank[0][n] + per_rank[1][n]) / 2
+            acc[n] = avg if n not in acc else acc[n] + avg
+    assert set(acc) == set(g0) == set(g1) and len(acc) > 30
+    for n in acc:
+        assert torch.equal(g0[n], g1[n]), n
+        assert torch.allclose(g0[n], acc[n], rtol=1e-5, atol=1e-7), n

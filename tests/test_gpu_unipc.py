@@ -44,7 +44,7 @@ def test_unipc_fused_trajectory_bit_exact(golden):
 def test_unipc_fused_vs_oracle_all_orders(n):
     """Every (corrector, predictor) order combination, ragged and full 720p latent sizes, against
     the oracle's torch chain on the CPU (forward and autograd backward): bit-exact."""
-    from prfl_amd import ops
+    from prfl_amd import custom_ops
     gen = torch.Generator().manual_seed(n)
     sample = torch.randn(n, generator=gen).to(torch.bfloat16)
     last = torch.randn(n, generator=gen).to(torch.bfloat16)
@@ -61,7 +61,7 @@ def test_unipc_fused_vs_oracle_all_orders(n):
                                            h1, h2 if corr == 2 else None, coef, corr, pred)
             (p_r.float() * gp).sum().backward()
             mo_g = mo.to(DEV).requires_grad_(True)
-            m_g, x_g, p_g = ops.unipc_step(mo_g, sample.to(DEV), last.to(DEV) if corr else None,
+            m_g, x_g, p_g = custom_ops.unipc_update(mo_g, sample.to(DEV), last.to(DEV) if corr else None,
                                            h1.to(DEV), h2.to(DEV) if corr == 2 else None, coef,
                                            corr, pred)
             (p_g.float() * gp.to(DEV)).sum().backward()
@@ -73,13 +73,13 @@ def test_unipc_fused_vs_oracle_all_orders(n):
 
 
 def test_unipc_fused_rejects_bad_inputs():
-    from prfl_amd import ops
+    from prfl_amd import custom_ops
     s = torch.zeros(64, dtype=torch.bfloat16, device=DEV)
     mo = torch.zeros(64, device=DEV)
     with pytest.raises(NotImplementedError):
-        ops.unipc_step(mo.bfloat16(), s, None, None, None, [0.0] * 11, 0, 1)
+        custom_ops.unipc_update(mo.bfloat16(), s, None, None, None, [0.0] * 11, 0, 1)
     with pytest.raises(RuntimeError):
-        ops.unipc_step(mo, s, None, None, None, [0.0] * 11, 0, 2)   # order 2 needs history
+        custom_ops.unipc_update(mo, s, None, None, None, [0.0] * 11, 0, 2)   # order 2 needs history
     with pytest.raises(NotImplementedError):
-        ops.unipc_step(mo, s.float().requires_grad_(True).bfloat16(), None, None, None,
+        custom_ops.unipc_update(mo, s.float().requires_grad_(True).bfloat16(), None, None, None,
                        [0.0] * 11, 0, 1)

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 
 import test_gpu_model as T  # noqa: E402
 from oracle import wan_oracle as O  # noqa: E402
-from prfl_amd import ops  # noqa: E402
+from prfl_amd import ops, custom_ops  # noqa: E402
 from prfl_amd.schedulers import FlowUniPCMultistepScheduler  # noqa: E402
 
 cache = {}
@@ -27,7 +27,7 @@ calls = []
 
 
 def spy(mo, sample, last, h1, h2, coef, corr, pred):
-    out = ops.unipc_step(mo, sample, last, h1, h2, coef, corr, pred)
+    out = custom_ops.unipc_update(mo, sample, last, h1, h2, coef, corr, pred)
     cl = lambda t: None if t is None else t.detach().clone()  # noqa: E731
     calls.append((cl(mo), cl(sample), cl(last), cl(h1), cl(h2), coef, corr, pred,
                   [cl(o) for o in out], mo.requires_grad))
@@ -50,7 +50,7 @@ for ci, (mo, s, last, h1, h2, coef, corr, pred, outs, rg) in enumerate(calls):
         gp = torch.randn(s.shape, generator=torch.Generator().manual_seed(ci)).to(dev)
         (ref[2].float() * gp).sum().backward()
         mo_f = mo.detach().clone().requires_grad_(True)
-        o2 = ops.unipc_step(mo_f, s, last, h1, h2, coef, corr, pred)
+        o2 = custom_ops.unipc_update(mo_f, s, last, h1, h2, coef, corr, pred)
         (o2[2].float() * gp.cuda()).sum().backward()
         gd = (mo_f.grad.cpu() - mo_r.grad.cpu()).abs().max().item()
         print(f"   vs oracle on {dev}: fwd max|d| m_t {d[0]:.3e} x_c {d[1]:.3e} prev {d[2]:.3e}; "
