@@ -346,6 +346,7 @@ def main():
                              else "Wan2.1-T2V-14B (40 blocks, C=5120)"), "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
         "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),
+        "stash_gb": stash_gb,
         "algorithmic_tflop_per_step": round(flops_it / 1e12, 1),
         "achieved_tflops_per_gpu": round(flops_it * steps / dt / 1e12, 1),
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 1),

@@ -15,7 +15,10 @@
 // fp32 row sum.  The workgroup's four waves merge in LDS; a second kernel merges the splits and
 // writes o (bf16) and the log2-domain LSE.
 //
-// Backward (FA2 recomputation, no atomics): D_h = do_h . o_h; per key p = exp2(s*sl2 - lse2),
+// Backward (recomputation, no atomics): D_h = do_h . o_h with the fp32 o the forward also writes
+// (NOT flash-attention's bf16 O: with one query over up to 74k nearly uniform keys, dp - D is a
+// cancellation and D from a bf16-rounded o costs the key-side gradient several % — the
+// reference's SDPA backward differentiates the unrounded output); per key p = exp2(s*sl2 - lse2),
 // dp = do_h . v, ds = p (dp - D); dk = scale ds q_h and dv = p do_h are written straight into
 // dkv [N][L][2E] (bf16, the in-projection's dY), dq_h += ds k accumulates per wave, merged per
 // workgroup into a split partial, summed by the merge kernel.
@@ -152,9 +155,11 @@ __global__ __launch_bounds__(PNT) void pool_fwd_kernel(PoolArgs a) {
   }
 }
 
-// o[n][h*hd + d] = bf16(sum_s part_o * 2^(m_s - M) / sum_s part_l * 2^(m_s - M)); lse2 = M + log2 L
+// o[n][h*hd + d] = bf16(sum_s part_o * 2^(m_s - M) / sum_s part_l * 2^(m_s - M)); lse2 = M + log2 L;
+// o32 (optional) = the same before the bf16 rounding
 __global__ __launch_bounds__(PNT) void pool_merge_kernel(PoolArgs a, bf16* __restrict__ o,
-                                                         int64_t ldo, float* __restrict__ lse2) {
+                                                         int64_t ldo, float* __restrict__ lse2,
+                                                         float* __restrict__ o32) {
   const int h = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * a.H + h) * a.nsplit;
   float M = -__builtin_huge_valf();
@@ -170,13 +175,14 @@ __global__ __launch_bounds__(PNT) void pool_merge_kernel(PoolArgs a, bf16* __res
       if (a.part_m[base + s] != -__builtin_huge_valf())
         acc += a.part_o[(base + s) * a.hd + d] * __builtin_amdgcn_exp2f(a.part_m[base + s] - M);
     o[(int64_t)n * ldo + h * a.hd + d] = f2bf(acc * inv);
+    if (o32) o32[(int64_t)n * a.E + h * a.hd + d] = acc * inv;
   }
   if (threadIdx.x == 0) lse2[(int64_t)n * a.H + h] = M + log2f(Ls);
 }
 
 struct PoolBwdArgs {
   PoolArgs f;
-  const bf16* dout; const bf16* o;   // [N][E]
+  const bf16* dout; const float* o32;   // [N][E]
   const float* lse2;                 // [N][H]
   bf16* dkv; int64_t lddkv, bdkv;
 };
@@ -199,13 +205,13 @@ __global__ __launch_bounds__(PNT) void pool_bwd_kernel(PoolBwdArgs b) {
       const int64_t off = (int64_t)n * a.ldq + h * a.hd + pc * 8;
       load8(a.q + off, qf[j]);
       load8(b.dout + off, df[j]);
-      float of[8];
-      load8(b.o + off, of);
+      const float* op = b.o32 + (int64_t)n * a.E + h * a.hd + pc * 8;
+      const f32x4 o0 = *(const f32x4*)op, o1 = *(const f32x4*)(op + 4);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dd += df[j][i] * of[i];
+      for (int i = 0; i < 4; ++i) dd += df[j][i] * o0[i] + df[j][i + 4] * o1[i];
     }
   }
-  dd = wave_sum(dd);                                   // D = rowsum(dO * O), bf16 O (FA2)
+  dd = wave_sum(dd);                                   // D = rowsum(dO * O), fp32 O
   const float lse = b.lse2[(int64_t)n * a.H + h];
   const bf16* kb = a.kv + (int64_t)n * a.bkv + h * a.hd;
   const bf16* vb = kb + a.E;
@@ -310,8 +316,9 @@ extern "C" int prfl_query_pool_splits(int64_t N, int64_t L, int64_t H) {
 
 extern "C" int prfl_query_pool_fwd(const void* q, int64_t ldq, const void* kv, int64_t ldkv,
                                    int64_t bkv, int64_t N, int64_t L, int64_t H, int64_t E,
-                                   float scale, void* o, int64_t ldo, float* lse2, float* part_m,
-                                   float* part_l, float* part_o, int64_t nsplit, void* stream) {
+                                   float scale, void* o, int64_t ldo, float* lse2, float* o32,
+                                   float* part_m, float* part_l, float* part_o, int64_t nsplit,
+                                   void* stream) {
   if (!pool_shape_ok(N, L, H, E, ldq, ldkv, q, kv) || nsplit <= 0 || nsplit > L)
     return (int)hipErrorInvalidValue;
   PoolArgs a{(const bf16*)q, ldq, (const bf16*)kv, ldkv, bkv, (int)N, (int)L, (int)H,
@@ -321,7 +328,7 @@ extern "C" int prfl_query_pool_fwd(const void* q, int64_t ldq, const void* kv, i
   prfl_prof::begin(KID_POOL, s);
   hipLaunchKernelGGL(pool_fwd_kernel, dim3(nsplit, H, N), dim3(PNT), 0, s, a);
   PRFL_LAUNCH_CHECK();
-  hipLaunchKernelGGL(pool_merge_kernel, dim3(H, N), dim3(PNT), 0, s, a, (bf16*)o, ldo, lse2);
+  hipLaunchKernelGGL(pool_merge_kernel, dim3(H, N), dim3(PNT), 0, s, a, (bf16*)o, ldo, lse2, o32);
   prfl_prof::set_work((double)N * L * 2 * E * 2);
   prfl_prof::end(KID_POOL, s);
   PRFL_LAUNCH_CHECK();
@@ -329,17 +336,17 @@ extern "C" int prfl_query_pool_fwd(const void* q, int64_t ldq, const void* kv, i
 }
 
 extern "C" int prfl_query_pool_bwd(const void* dout, const void* q, int64_t ldq, const void* kv,
-                                   int64_t ldkv, int64_t bkv, const void* o, const float* lse2,
+                                   int64_t ldkv, int64_t bkv, const float* o32, const float* lse2,
                                    int64_t N, int64_t L, int64_t H, int64_t E, float scale,
                                    float* dq, int64_t lddq, void* dkv, int64_t lddkv, int64_t bdkv,
                                    float* part_o, int64_t nsplit, void* stream) {
   if (!pool_shape_ok(N, L, H, E, ldq, ldkv, q, kv) || nsplit <= 0 || nsplit > L ||
-      lddkv % 8 || ((uintptr_t)dkv & 15) || ((uintptr_t)dout & 15) || ((uintptr_t)o & 15))
+      lddkv % 8 || ((uintptr_t)dkv & 15) || ((uintptr_t)dout & 15) || ((uintptr_t)o32 & 15))
     return (int)hipErrorInvalidValue;
   PoolArgs a{(const bf16*)q, ldq, (const bf16*)kv, ldkv, bkv, (int)N, (int)L, (int)H,
              (int)(E / H), (int)E, scale * 1.4426950408889634f, scale, (int)nsplit,
              (int)((L + nsplit - 1) / nsplit), nullptr, nullptr, part_o};
-  PoolBwdArgs b{a, (const bf16*)dout, (const bf16*)o, lse2, (bf16*)dkv, lddkv, bdkv};
+  PoolBwdArgs b{a, (const bf16*)dout, o32, lse2, (bf16*)dkv, lddkv, bdkv};
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_POOL, s);
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(nsplit, H, N), dim3(PNT), 0, s, b);

@@ -44,7 +44,8 @@ SIGNATURES = {
     "prfl_unipc_step": [P, P, P, P, P, P, P, P, I64, P, I32, I32, P],
     "prfl_unipc_step_bwd": [P, P, I64, P, I32, I32, P],
     "prfl_query_pool_splits": [I64, I64, I64],
-    "prfl_query_pool_fwd": [P, I64, P, I64, I64, I64, I64, I64, I64, F32, P, I64, P, P, P, P, I64, P],
+    "prfl_query_pool_fwd": [P, I64, P, I64, I64, I64, I64, I64, I64, F32, P, I64, P, P, P, P, P, I64,
+                            P],
     "prfl_query_pool_bwd": [P, P, I64, P, I64, I64, P, P, I64, I64, I64, I64, F32, P, I64, P, I64,
                             I64, P, I64, P],
     "prfl_prof_enable": [I32],

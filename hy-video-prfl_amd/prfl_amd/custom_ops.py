@@ -311,43 +311,46 @@ flash_attention.register_autograd(_fa_bwd, setup_context=_fa_setup)
 
 # ================================================= single-query pooling (reward head) ====
 @torch.library.custom_op("prfl::query_pool", mutates_args=(), device_types="cuda")
-def query_pool(q: Tensor, kv: Tensor, num_heads: int, scale: float) -> Tuple[Tensor, Tensor]:
+def query_pool(q: Tensor, kv: Tensor, num_heads: int, scale: float) -> Tuple[Tensor, Tensor, Tensor]:
     """softmax(q k^T * scale) v per head for ONE query per sample: q [N, E] bf16, kv [N, L, 2E]
-    bf16 (k | v, the MHA in-projection output) -> (o bf16 [N, E], lse2 fp32 [N, H])."""
+    bf16 (k | v, the MHA in-projection output) -> (o bf16 [N, E], lse2 fp32 [N, H], o32 fp32
+    [N, E]: o before its bf16 rounding, kept for the backward's D)."""
     return ops.query_pool_fwd(q.contiguous(), kv, num_heads, scale)
 
 
 @query_pool.register_fake
 def _(q, kv, num_heads, scale):
-    return q.new_empty(q.shape, dtype=BF16), q.new_empty((q.shape[0], num_heads), dtype=F32)
+    return (q.new_empty(q.shape, dtype=BF16), q.new_empty((q.shape[0], num_heads), dtype=F32),
+            q.new_empty(q.shape, dtype=F32))
 
 
 @torch.library.custom_op("prfl::query_pool_backward", mutates_args=(), device_types="cuda")
-def query_pool_backward(do: Tensor, q: Tensor, kv: Tensor, o: Tensor, lse: Tensor, num_heads: int,
-                        scale: float) -> Tuple[Tensor, Tensor]:
+def query_pool_backward(do: Tensor, q: Tensor, kv: Tensor, o32: Tensor, lse: Tensor,
+                        num_heads: int, scale: float) -> Tuple[Tensor, Tensor]:
     """(dq fp32 [N, E], dkv bf16 [N, L, 2E])."""
-    return ops.query_pool_bwd(do.to(BF16).contiguous(), q.contiguous(), kv, o, lse, num_heads, scale)
+    return ops.query_pool_bwd(do.to(BF16).contiguous(), q.contiguous(), kv, o32, lse, num_heads,
+                              scale)
 
 
 @query_pool_backward.register_fake
-def _(do, q, kv, o, lse, num_heads, scale):
+def _(do, q, kv, o32, lse, num_heads, scale):
     return q.new_empty(q.shape, dtype=F32), torch.empty_like(kv)
 
 
 def _qp_setup(ctx, inputs, output):
     q, kv, num_heads, scale = inputs
-    o, lse = output
-    ctx.mark_non_differentiable(lse)
+    o, lse, o32 = output
+    ctx.mark_non_differentiable(lse, o32)
     ctx.set_materialize_grads(False)
-    ctx.save_for_backward(q, kv, o, lse)
+    ctx.save_for_backward(q, kv, o32, lse)
     ctx.args = (num_heads, scale)
 
 
-def _qp_bwd(ctx, do, _dlse):
-    q, kv, o, lse = ctx.saved_tensors
+def _qp_bwd(ctx, do, _dlse, _do32):
+    q, kv, o32, lse = ctx.saved_tensors
     if do is None:
         return None, None, None, None
-    dq, dkv = query_pool_backward(do.contiguous(), q, kv, o, lse, *ctx.args)
+    dq, dkv = query_pool_backward(do.contiguous(), q, kv, o32, lse, *ctx.args)
     return dq.to(q.dtype), dkv, None, None
 
 

@@ -244,7 +244,7 @@ def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=No
 
 def query_pool_fwd(q, kv, num_heads, scale, nsplit=None):
     """Single-query attention pooling (csrc/pool.hip): q [N, E] bf16, kv [N, L, 2E] bf16 (k | v)
-    -> (o bf16 [N, E], lse2 fp32 [N, H])."""
+    -> (o bf16 [N, E], lse2 fp32 [N, H], o32 fp32 [N, E] = o before its bf16 rounding)."""
     _lib.require_gpu(q, kv)
     assert q.dtype == BF16 and kv.dtype == BF16 and kv.stride(2) == 1
     N, E = q.shape
@@ -254,16 +254,17 @@ def query_pool_fwd(q, kv, num_heads, scale, nsplit=None):
     hd = E // num_heads
     o = torch.empty(N, E, dtype=BF16, device=q.device)
     lse = torch.empty(N, num_heads, dtype=torch.float32, device=q.device)
+    o32 = torch.empty(N, E, dtype=torch.float32, device=q.device)
     pm = torch.empty(N * num_heads * nsplit, dtype=torch.float32, device=q.device)
     pl = torch.empty_like(pm)
     po = torch.empty(N * num_heads * nsplit * hd, dtype=torch.float32, device=q.device)
     call("prfl_query_pool_fwd", ptr(q), I64(_ld(q)), ptr(kv), I64(kv.stride(1)), I64(kv.stride(0)),
-         I64(N), I64(L), I64(num_heads), I64(E), F32(scale), ptr(o), I64(E), ptr(lse), ptr(pm),
-         ptr(pl), ptr(po), I64(nsplit), stream_ptr())
-    return o, lse
+         I64(N), I64(L), I64(num_heads), I64(E), F32(scale), ptr(o), I64(E), ptr(lse), ptr(o32),
+         ptr(pm), ptr(pl), ptr(po), I64(nsplit), stream_ptr())
+    return o, lse, o32
 
 
-def query_pool_bwd(do, q, kv, o, lse, num_heads, scale, nsplit=None):
+def query_pool_bwd(do, q, kv, o32, lse, num_heads, scale, nsplit=None):
     """-> (dq fp32 [N, E], dkv bf16 [N, L, 2E])."""
     N, E = q.shape
     L = kv.shape[1]
@@ -274,7 +275,7 @@ def query_pool_bwd(do, q, kv, o, lse, num_heads, scale, nsplit=None):
     dkv = torch.empty(N, L, 2 * E, dtype=BF16, device=q.device)
     po = torch.empty(N * num_heads * nsplit * hd, dtype=torch.float32, device=q.device)
     call("prfl_query_pool_bwd", ptr(do), ptr(q), I64(_ld(q)), ptr(kv), I64(kv.stride(1)),
-         I64(kv.stride(0)), ptr(o), ptr(lse), I64(N), I64(L), I64(num_heads), I64(E), F32(scale),
+         I64(kv.stride(0)), ptr(o32), ptr(lse), I64(N), I64(L), I64(num_heads), I64(E), F32(scale),
          ptr(dq), I64(E), ptr(dkv), I64(2 * E), I64(L * 2 * E), ptr(po), I64(nsplit), stream_ptr())
     return dq, dkv
 

@@ -77,18 +77,20 @@ int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
  * (diffusers_lite/utils/network.py:80; num_queries 1, 8 heads, E = 5120): per sample n and head
  * h, o[n][h*hd:(h+1)*hd] = softmax_l(q_h . k_{l,h} * scale) V_{l,h}, hd = E / H (hd % 8 == 0,
  * hd <= 1024).  q [N][ldq] bf16; kv [N][L][ldkv] bf16 with K in columns [0, E) and V in
- * [E, 2E) (the in-projection output), sample stride bkv.  Split over L into nsplit parts
+ * [E, 2E) (the in-projection output), sample stride bkv.  o32 (optional, [N][E] fp32) receives
+ * the output before its bf16 rounding (the backward's D).  Split over L into nsplit parts
  * (prfl_query_pool_splits gives the default); part_m / part_l [N*H*nsplit] and part_o
  * [N*H*nsplit*hd] fp32 are caller-owned workspace.  lse2 [N][H] = log2-domain LSE. */
 int prfl_query_pool_splits(int64_t N, int64_t L, int64_t H);
 int prfl_query_pool_fwd(const void* q, int64_t ldq, const void* kv, int64_t ldkv, int64_t bkv,
                         int64_t N, int64_t L, int64_t H, int64_t E, float scale, void* o,
-                        int64_t ldo, float* lse2, float* part_m, float* part_l, float* part_o,
-                        int64_t nsplit, void* stream);
+                        int64_t ldo, float* lse2, float* o32, float* part_m, float* part_l,
+                        float* part_o, int64_t nsplit, void* stream);
 /* Backward: dq fp32 [N][lddq] (= scale * sum_l ds k), dkv bf16 [N][L][lddkv] (dK | dV, every
- * row written), part_o [N*H*nsplit*hd] workspace; dout, o bf16 [N][ldq]. */
+ * row written), part_o [N*H*nsplit*hd] workspace; dout bf16 [N][ldq]; o32 = the forward's fp32
+ * output [N][E] (D = rowsum(dout * o32)). */
 int prfl_query_pool_bwd(const void* dout, const void* q, int64_t ldq, const void* kv,
-                        int64_t ldkv, int64_t bkv, const void* o, const float* lse2, int64_t N,
+                        int64_t ldkv, int64_t bkv, const float* o32, const float* lse2, int64_t N,
                         int64_t L, int64_t H, int64_t E, float scale, float* dq, int64_t lddq,
                         void* dkv, int64_t lddkv, int64_t bdkv, float* part_o, int64_t nsplit,
                         void* stream);

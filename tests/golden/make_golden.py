@@ -334,6 +334,8 @@ def case_toy_pavrm():
             prob = NET.forward_mlp(mlp, pooled)
         lab = torch.tensor([label])
         loss = crit(prob.squeeze().float(), lab.squeeze().float())
+        states = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in (lrm, qa, mlp)]
+        out.update(_toy_pavrm_fp32_truth(s, states, noisy, fm.timesteps[[idx]], ctx, lab))
         loss.backward()
         g = {f"s{s}:" + k: v for k, v in grads_of(lrm).items()}
         g.update({f"s{s}:qa." + k: v for k, v in grads_of(qa).items()})
@@ -346,6 +348,53 @@ def case_toy_pavrm():
                     f"s{s}:prob": np32(prob), f"s{s}:loss": np32(loss),
                     f"s{s}:grad_norm": np32(gn), **g})
     save("toy_pavrm", **out)
+
+
+def _exact_attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=None,
+                     q_scale=None, causal=False, window_size=(-1, -1), deterministic=False,
+                     dtype=None, version=None):
+    """Unrounded attention in the inputs' dtype (fp32) for the truth run."""
+    if q_scale is not None:
+        q = q * q_scale
+    scale = softmax_scale if softmax_scale is not None else q.size(-1) ** -0.5
+    s = torch.einsum("blnd,bmnd->bnlm", q, k) * scale
+    if k_lens is not None:
+        lk = k.shape[1]
+        s = s.masked_fill(torch.arange(lk).view(1, 1, 1, lk) >= k_lens.view(-1, 1, 1, 1), float("-inf"))
+    return torch.einsum("bnlm,bmnd->blnd", torch.softmax(s, -1), v)
+
+
+def _toy_pavrm_fp32_truth(step, states, noisy, timestep, ctx, label):
+    """Step `step` of case_toy_pavrm from the same weights and inputs without autocast, all fp32,
+    with unrounded attention: the gradients the bf16 runs approximate (fp32 rounding ~1e-7 vs
+    bf16's ~4e-3).  The GPU test holds our error to this truth next to the reference's own."""
+    saved = M.flash_attention
+    M.flash_attention = _exact_attention
+    try:
+        lrm = _toy_model("t2v")
+        del lrm.head
+        lrm.head = None
+        qa = NET.QueryAttention(256, 1, 8, 0., return_type="query")
+        mlp = NET.MLP(256)
+        for m, st in zip((lrm, qa, mlp), states):
+            m.load_state_dict(st)
+        for name in ("patch_embedding", "text_embedding", "time_embedding", "time_projection"):
+            for p in getattr(lrm, name).parameters():
+                p.requires_grad_(False)
+        feats = DU.list2batch(lrm(x=DU.batch2list(noisy.float()), t=timestep,
+                                  context=DU.batch2list(ctx.float()), seq_len=105,
+                                  output_features=True, selected_layers=[2]))
+        prob = NET.forward_mlp(mlp, qa(feats))
+        loss = torch.nn.BCELoss()(prob.squeeze(), label.squeeze().float())
+        loss.backward()
+        pre = f"s{step}:t32:"
+        g = {pre + k: v for k, v in grads_of(lrm).items()}
+        g.update({pre + "qa." + k: v for k, v in grads_of(qa).items()})
+        g.update({pre + "mlp." + k: v for k, v in grads_of(mlp).items()})
+        g[pre + "prob"] = np.float64(prob.item())
+        return g
+    finally:
+        M.flash_attention = saved
 
 
 if __name__ == "__main__":

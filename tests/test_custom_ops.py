@@ -55,10 +55,10 @@ def test_fake_shapes(cops):
         g = torch.ops.prfl.wan_block_backward(out, x, e, ctx, params, ao, lse, 2, [3, 5, 7], [105],
                                               tab, False, 1e-6, False, True, True)
         assert [t.shape for t in g[3:]] == [p.shape for p in params] and g[2].shape == ctx.shape
-        o, l2 = torch.ops.prfl.query_pool(torch.empty(2, 5120, device=dev, dtype=torch.bfloat16),
+        o, l2, o32 = torch.ops.prfl.query_pool(torch.empty(2, 5120, device=dev, dtype=torch.bfloat16),
                                           torch.empty(2, 77, 10240, device=dev, dtype=torch.bfloat16),
                                           8, 0.04)
-        assert o.shape == (2, 5120) and l2.shape == (2, 8)
+        assert o.shape == (2, 5120) and l2.shape == (2, 8) and o32.dtype == torch.float32
         y, pre = torch.ops.prfl.linear_bf16(x, torch.empty(512, 256, device=dev), None, True)
         assert y.shape == (1, 105, 512) and pre.shape == (105, 512)
 

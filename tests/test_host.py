@@ -113,3 +113,23 @@ def test_bench_stash_only_where_moments_leave_hbm():
             for w in ("prfl_t2v_720", "prfl_i2v_720", "prfl_t2v_480", "pavrm_t2v_480")}
     assert fits == {"prfl_t2v_720": True, "prfl_i2v_720": True, "prfl_t2v_480": False,
                     "pavrm_t2v_480": False}
+
+
+def test_720p_data_parallel_memory_plan_fits():
+    """The N = 8 plan at 720p x 81f (tools/memory_plan.py; unmeasured on hardware): the analytic
+    per-rank budget and the N = 1 measurement adjusted to the N > 1 stash (20 GB) plus an RCCL
+    buffer bound both leave room on the 288 GiB card."""
+    import glob
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import memory_plan as mp
+    rows = mp.analytic(8, 20.0)
+    assert rows["RCCL buffers"] > 0 and sum(rows.values()) < 0.9 * mp.CARD_GB
+    runs = sorted(glob.glob(os.path.join(root, "profiles", "r0*_bench_prfl720_*.json")))
+    runs = [r for r in runs if json.load(open(r)).get("n_gpus") == 1
+            and json.load(open(r)).get("config", {}).get("latent") == [16, 21, 88, 160]]
+    assert runs
+    alloc, res = mp.from_measurement(8, 20.0, runs[-1])
+    assert res < mp.CARD_GB - 20, (runs[-1], alloc, res)

@@ -53,6 +53,35 @@ elif which == "ln":
               r.double().sum().item())
         print(f"ln_mod_fwd {name} {L}x{C}: {dt*1e3:.3f} ms  {L*C*6/dt/1e9:.0f} GB/s  checksum {ck}",
               flush=True)
+elif which == "gemm720":
+    # one dispatch per GEMM of a 720p block's forward + backward (the bench's shapes), for PMC runs
+    Lq = L
+    shapes = [("qkv", Lq, 3 * C, C), ("o", Lq, C, C), ("ffn1", Lq, F, C), ("ffn2", Lq, C, F)]
+    for name, M, N, K in shapes:
+        x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        for i in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            y = ops.linear(x, w)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"gemm fwd {name} {M}x{N}x{K} {dt*1e3:.2f} ms  {2*M*N*K/dt/1e12:.0f} TF/s", flush=True)
+        dy = (torch.randn(M, N, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        for i in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            ops.linear_dx(dy, w)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"gemm dx  {name} {M}x{K}x{N} {dt*1e3:.2f} ms  {2*M*N*K/dt/1e12:.0f} TF/s", flush=True)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            ops.linear_dw(dy, x)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"gemm dw  {name} {N}x{K}x{M} {dt*1e3:.2f} ms  {2*M*N*K/dt/1e12:.0f} TF/s", flush=True)
+        del x, w, y, dy
 elif which == "gemmfwd":
     # the forward projections of one block at L tokens (the rollout's hot GEMMs), bf16 epilogue
     for (N, K, name) in [(3 * C, C, "qkv"), (C, C, "o/cq/co"), (F, C, "ffn1"), (C, F, "ffn2")]:
