@@ -32,6 +32,7 @@ struct AttnArgs {
   float* LSE;            // [B][H][Lq], log2 domain
   int Lq, Lk, H, k_len;
   float sl2;             // softmax_scale * log2(e)
+  int B;
 };
 
 struct AttnBwdArgs {
@@ -46,6 +47,7 @@ struct AttnBwdArgs {
   bf16* dV; int64_t lddv, bdv;
   int Lq, Lk, H, k_len;
   float sl2, scale;
+  int B;
 };
 
 // LDS images (256-B rows of 128 bf16):
@@ -83,6 +85,29 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
                   f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
 }
 
+// XCD-aware (sample, head) grouping of a 1-D grid of ntile * nbh workgroups (tile = a 256-row
+// query or key block of one (sample, head)).  Workgroups b, b + 8, ... share an XCD (observed
+// round-robin dispatch; speed only, any placement stays correct), so give each XCD a disjoint
+// set of nbh / 8 (sample, head) pairs and walk all tiles of one pair before the next: the
+// ~32 workgroups an XCD runs at once then sweep the SAME head's K/V in near lockstep and hit in
+// that XCD's L2, instead of every XCD streaming every head from the fabric.  Bijective;
+// nbh % 8 != 0 keeps the plain order.  Measured at 720p x 81f (tools/ab_attn.py, one box, six
+// interleaved rounds, profiles/r02_ab_attn_xcd.txt): forward L2-miss traffic 30.4 -> 17.6 GB
+// per launch (FETCH_SIZE x 2), time 98.59 -> 98.34 ms (unchanged: the kernel is not memory
+// bound); the same grouping made dK/dV + dQ 2.3 % SLOWER, so the backward kernels keep the plain
+// (tile, head, sample) grid.
+__device__ __forceinline__ void xcd_tile(int ntile, int nbh, int& bh, int& tile) {
+  const int bid = blockIdx.x;
+  if ((nbh & 7) == 0) {
+    const int i = bid >> 3, per = nbh >> 3;
+    bh = (bid & 7) * per + i / ntile;
+    tile = i % ntile;
+  } else {
+    bh = bid / ntile;
+    tile = bid % ntile;
+  }
+}
+
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -114,7 +139,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
   constexpr int SB = 2 * SV;                   // bytes of one [K | V] ring stage
   __shared__ __attribute__((aligned(16))) char smem[3 * SB];   // ring of [K | V] tiles
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  int bh, tile;
+  xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile);
+  const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gp = w >> 2;
@@ -606,14 +633,16 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || (ldq | ldk | ldv | ldo) % 8)
     return (int)hipErrorInvalidValue;
-  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535) return (int)hipErrorInvalidValue;
+  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535 ||
+      ((Lq + 255) / 256) * H * B > 0x7fffffff || ((Lk + 255) / 256) * H * B > 0x7fffffff)
+    return (int)hipErrorInvalidValue;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f};
+             scale * 1.4426950408889634f, (int)B};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
-  const dim3 grid((Lq + 255) / 256, H, B);
+  const dim3 grid((unsigned)(((Lq + 255) / 256) * H * B));
   if (kid == KID_ATTN_FWD)
     hipLaunchKernelGGL((attn_fwd_kernel<false, 2, 3>), grid, dim3(512), 0, s, a);
   else
@@ -638,7 +667,9 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
       !aligned16(dq) || !aligned16(dk) || !aligned16(dv) ||
       (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8)
     return (int)hipErrorInvalidValue;
-  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535) return (int)hipErrorInvalidValue;
+  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535 ||
+      ((Lq + 255) / 256) * H * B > 0x7fffffff || ((Lk + 255) / 256) * H * B > 0x7fffffff)
+    return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrows = B * Lq * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((nrows + 15) / 16), dim3(256), 0, s,
@@ -648,7 +679,7 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
   AttnBwdArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
-                scale * 1.4426950408889634f, scale};
+                scale * 1.4426950408889634f, scale, (int)B};
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 255) / 256, H, B), dim3(512), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);

@@ -1,0 +1,82 @@
+"""A/B of two builds of the attention kernels in ONE process, interleaved (guide §5.4 rule 24):
+    python tools/ab_attn.py <libA.so> <libB.so> [L] [rounds]
+Times prfl_attn_fwd / prfl_attn_bwd at L tokens, 40 heads (720p: L = 73 920) with HIP events on
+the launch stream, checks that both builds give bit-identical outputs, and prints per-round
+times and the medians."""
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+P, I64, F32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float
+FWD = [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, F32, P]
+BWD = [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64, I64, P, I64,
+       I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P]
+
+
+def load(path):
+    lib = ctypes.CDLL(os.path.abspath(path))
+    lib.prfl_attn_fwd.argtypes, lib.prfl_attn_fwd.restype = FWD, ctypes.c_int
+    lib.prfl_attn_bwd.argtypes, lib.prfl_attn_bwd.restype = BWD, ctypes.c_int
+    return lib
+
+
+def main():
+    libs = [load(sys.argv[1]), load(sys.argv[2])]
+    L = int(sys.argv[3]) if len(sys.argv) > 3 else 73920
+    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 6
+    H, C = 40, 5120
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    qkv = torch.randn(L, 3 * C, generator=g, device=dev).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    do = torch.randn(L, C, generator=g, device=dev).to(torch.bfloat16)
+    outs = []
+    for _ in libs:
+        outs.append(dict(o=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
+                         lse=torch.empty(H, L, device=dev), delta=torch.empty(H, L, device=dev),
+                         dq=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
+                         dk=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
+                         dv=torch.empty(L, C, dtype=torch.bfloat16, device=dev)))
+    sc = 128 ** -0.5
+    st = torch.cuda.current_stream().cuda_stream
+
+    def fwd(lib, b):
+        rc = lib.prfl_attn_fwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                               b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc, st)
+        assert rc == 0
+
+    def bwd(lib, b):
+        rc = lib.prfl_attn_bwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                               b["o"].data_ptr(), C, 0, do.data_ptr(), C, 0, b["lse"].data_ptr(),
+                               b["delta"].data_ptr(), b["dq"].data_ptr(), C, 0, b["dk"].data_ptr(), C, 0,
+                               b["dv"].data_ptr(), C, 0, 1, L, L, H, L, sc, st)
+        assert rc == 0
+
+    times = {(i, w): [] for i in range(2) for w in ("fwd", "bwd")}
+    for r in range(rounds + 1):
+        for i, lib in enumerate(libs):
+            for w, fn in (("fwd", fwd), ("bwd", bwd)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(lib, outs[i])
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    times[(i, w)].append(e0.elapsed_time(e1))
+        if r:
+            print(f"round {r}: " + "  ".join(f"{'AB'[i]}-{w} {times[(i, w)][-1]:.2f} ms"
+                                           for i in range(2) for w in ("fwd", "bwd")), flush=True)
+    same = all(torch.equal(outs[0][n], outs[1][n]) for n in ("o", "lse", "dq", "dk", "dv"))
+    fl = {"fwd": 4 * L * L * C, "bwd": 14 * L * L * C}
+    for w in ("fwd", "bwd"):
+        ma, mb = statistics.median(times[(0, w)]), statistics.median(times[(1, w)])
+        print(f"{w}: A median {ma:.2f} ms ({fl[w] / ma / 1e9:.0f} TF/s)  B median {mb:.2f} ms "
+              f"({fl[w] / mb / 1e9:.0f} TF/s)  A/B time {ma / mb:.4f}")
+    print("bit-identical outputs:", same)
+
+
+if __name__ == "__main__":
+    main()
