@@ -71,6 +71,39 @@ __device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds_dst) {
       : "memory");
 }
 
+// LDS-DMA through a buffer resource: global address = SRD base + voffset (per lane) + soffset
+// (wave-uniform), so a loop that walks K moves only the SGPR soffset and keeps per-lane
+// offsets that are computed once (no per-load 64-bit address arithmetic on the VALU).
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+// raw buffer over [base, base + bytes): stride 0, dword3 = the gfx9 default data format
+__device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return (i32x4){(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
+                 (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu),
+                 (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000};
+}
+__device__ __forceinline__ void dma16_buf(i32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(__builtin_amdgcn_readfirstlane(lds_dst)),
+        "s"(__builtin_amdgcn_readfirstlane(soff))
+      : "memory");
+}
+
+// A wave-uniform pointer laundered through readfirstlane (SGPRs): `uniform_ptr(base + t * stride)
+// + lane_offset` then cannot be re-associated into a per-lane 64-bit `base + lane_offset` that
+// LICM hoists out of the tile loop (one VGPR pair per DMA stream -> spills at 256 VGPRs).
+template <typename T>
+__device__ __forceinline__ const T* uniform_ptr(const T* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }

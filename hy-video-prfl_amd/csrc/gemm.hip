@@ -494,6 +494,165 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------- 256x256, four waves, one wave per SIMD ---
+// The 256x256 tile on 4 waves (2 x 2), each wave 128x128 = 8x8 MFMA 16x16x32 tiles: 256 fp32
+// accumulators per lane (the AGPR half of the 512-entry register file at one wave per SIMD) and
+// half the LDS read bytes per MFMA of the 8-wave kernel (16 fragments feed 64 MFMAs).  With no
+// partner wave on the SIMD, each wave overlaps its own fragment reads with its MFMAs: the
+// fragments of K-slice j+1 (32 deep) are read while the 64 MFMAs of slice j run.
+// K-slices of 32 land by LDS-DMA in a 4-slot ring (slot = A 16 KiB | B 16 KiB):
+//   iteration j: counted vmcnt (own DMA of slice j+1 done) -> barrier M_j -> issue slice j+3
+//   into slot (j+3)%4 = (j-1)%4 -> MFMAs of slice j || reads of slice j+1.
+// RAW: slice j+1 is read only after M_j, which every wave passes after retiring its own part of
+// it.  WAR: slot (j-1)%4 was last read (slice j-1's fragments) before iteration j-1's MFMAs
+// consumed them, i.e. before every wave's M_j.  DMA latency budget: 3 slices (~3 x 1024 MFMA
+// cycles) per slice.
+// K-major slice image: [256 rows][32 k], 64-B rows, 16-B chunk c of row r at position
+// c ^ ((r >> 2) & 2) (conflict-free for the 16x16x32 fragment read: the four row quads of a
+// b128 lane group land on four different chunk columns).  MN-major slice image: two [32 k][128]
+// halves with 256-B rows and the swz_mn granule swizzle of the 128 kernel.
+constexpr int BK4 = 32, SLICE4 = 32768, HALF4 = 16384;
+#ifndef GEMM4W_ASM
+#define GEMM4W_ASM 1
+#endif
+#ifndef GEMM4W_SB
+#define GEMM4W_SB 1
+#endif
+
+__device__ __forceinline__ int kc_pos(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 2)) << 4); }
+
+// byte offset (from the operand's SRD base: the tile's first row for K-major, its first column
+// for MN-major) of this lane's 16 B of piece i (< 4) of the wave's quarter of a slice at k0 = 0
+template <bool KC>
+__device__ __forceinline__ uint32_t piece_off4(int64_t ld, int wid, int lane, int i) {
+  const int piece = wid * 4 + i;                       // 16 pieces of 1 KiB per operand
+  if (KC) {          // 16 rows x 64 B per piece
+    const int row = piece * 16 + (lane >> 2), pos = lane & 3;
+    return (uint32_t)(row * ld * 2) + ((pos ^ ((row >> 2) & 2)) << 4);
+  }
+  // half piece>>3, 4 k-rows x 256 B per piece
+  const int kr = (piece & 7) * 4 + (lane >> 4), pb = (lane & 15) << 4;
+  const int lc = (pb ^ (swz_mn(kr) << 5)) >> 1;
+  return (uint32_t)(kr * ld * 2) + (uint32_t)(((piece >> 3) * 128 + lc) * 2);
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag4(const char* lds, int base, int lane) {
+  if (KC) return *(const bf16x8*)(lds + kc_pos(base + (lane & 15), lane >> 4));
+  return read_frag<false>(lds + (base >> 7) * 8192, base & 127, 0, lane);
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
+  int tm, tn;
+  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // ns = K / 32 is even and >= 4 (host check).  Branch-free body: past the last slice the DMA
+  // re-fetches slice ns-1 into the free slot and the reads fetch fragments nobody uses, so every
+  // iteration issues the same 8 DMA instructions per wave and `vmcnt(8)` is always the count
+  const int ns = g.K / BK4;
+  // operand SRDs (host guarantees every byte offset fits 32 bits); K-major rows past the
+  // operand's end are out of the SRD's range and load zeros
+  const i32x4 srd_a = A_KC ? make_srd(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(g.M - m0) * g.lda * 2))
+                           : make_srd(g.A + m0, (uint32_t)((int64_t)g.K * g.lda * 2 - (int64_t)m0 * 2));
+  const i32x4 srd_b = B_KC ? make_srd(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(g.N - n0) * g.ldb * 2))
+                           : make_srd(g.B + n0, (uint32_t)((int64_t)g.K * g.ldb * 2 - (int64_t)n0 * 2));
+  uint32_t offa[4], offb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i);
+    offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i);
+  }
+  // k0 -> soffset: 2 B per k for K-major operands, one row (ld elements) per k for MN-major
+  auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
+  auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
+  auto issue = [&](int j) {
+    j = min(j, ns - 1);
+    char* st = smem + (j & 3) * SLICE4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_buf(srd_a, offa[i], soff_a(j), lds_addr(st + (wid * 4 + i) * 1024));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dma16_buf(srd_b, offb[i], soff_b(j), lds_addr(st + HALF4 + (wid * 4 + i) * 1024));
+  };
+  auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+    const char* st = smem + (j & 3) * SLICE4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bf[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
+  };
+  auto step = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own part of slice j+1 landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int jd = min(j + 3, ns - 1);
+    char* sd = smem + ((j + 3) & 3) * SLICE4;
+    const char* st = smem + ((j + 1) & 3) * SLICE4;
+    // eight chunks: row i's 8 MFMAs beside one LDS-DMA piece of slice j+3 and the reads of
+    // fragments i of slice j+1, pinned in place by sched_barrier so the non-MFMA work spreads
+    // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < 4) dma16_buf(srd_a, offa[i], soff_a(jd), lds_addr(sd + (wid * 4 + i) * 1024));
+      else dma16_buf(srd_b, offb[i - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + i - 4) * 1024));
+      na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
+      nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+#if GEMM4W_ASM
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][jj]) : "v"(cb[jj]), "v"(ca[i]));
+#else
+        acc[i][jj] = mfma16(cb[jj], ca[i], acc[i][jj]);
+#endif
+      }
+#if GEMM4W_SB
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+  };
+
+  asm volatile("s_nop 7" ::: "memory");    // accumulator zeroing (VALU) -> first asm MFMA
+  issue(0);
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 fa[8], fb[8], ga[8], gb[8];
+  read(0, fa, fb);
+  for (int j = 0; j < ns; j += 2) {
+    step(j, fa, fb, ga, gb);
+    step(j + 1, ga, gb, fa, fb);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the MFMAs are inline asm: the compiler does not see their AGPR writes, so pad the
+  // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
+    }
+  }
+}
+
 // tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced
 // (parity tests: both kernels accumulate every element in the same k order, so their outputs
 // are bit-identical)
@@ -501,8 +660,16 @@ template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
   const bool fits256 = (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) && (B_KC || g.N % BN2 == 0);
-  if (tile == 256 && !fits256) return (int)hipErrorInvalidValue;
-  if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
+  if ((tile == 256 || tile == 4) && !fits256) return (int)hipErrorInvalidValue;
+  // the four-wave kernel addresses each operand through a 32-bit buffer offset
+  const int64_t bytes_a = (A_KC ? (int64_t)g.M : (int64_t)g.K) * g.lda * 2;
+  const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
+  const bool fits4w = fits256 && (g.K % 64) == 0 && g.K >= 128 && bytes_a < (1ll << 32) &&
+                      bytes_b < (1ll << 32);
+  if (tile == 4 && !fits4w) return (int)hipErrorInvalidValue;
+  if (tile == 4) {
+    hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
+  } else if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
     hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
   } else {
     const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
@@ -521,7 +688,7 @@ extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, co
                                     void* aux, int64_t ldaux, int accumulate, int tile,
                                     void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (tile != 0 && tile != 128 && tile != 256) return (int)hipErrorInvalidValue;
+  if (tile != 0 && tile != 128 && tile != 256 && tile != 4) return (int)hipErrorInvalidValue;
   // K is a contiguous extent only for K-major operands; MN-major operands take any K (row tail)
   if (K <= 0 || ((a_kmajor || b_kmajor) && (K % 8) != 0) || (N % 4) != 0)
     return (int)hipErrorInvalidValue;

@@ -82,6 +82,17 @@ elif which == "gemm720":
             dt = time.time() - t0
             print(f"gemm dw  {name} {N}x{K}x{M} {dt*1e3:.2f} ms  {2*M*N*K/dt/1e12:.0f} TF/s", flush=True)
         del x, w, y, dy
+elif which == "gemmcmp":
+    # the QKV forward GEMM through prfl_gemm and through torch.matmul (hipBLASLt), same operands:
+    # PMC comparison of MFMA busy, clock (GRBM_GUI_ACTIVE / 8 / wall) and instruction mix
+    x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(3 * C, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    y = torch.empty(L, 3 * C, device=dev, dtype=torch.bfloat16)
+    for i in range(reps):
+        ops.linear(x, w, out=y)
+        torch.matmul(x, w.t(), out=y)
+    torch.cuda.synchronize()
+    print("gemmcmp done", flush=True)
 elif which == "gemmfwd":
     # the forward projections of one block at L tokens (the rollout's hot GEMMs), bf16 epilogue
     for (N, K, name) in [(3 * C, C, "qkv"), (C, C, "o/cq/co"), (F, C, "ffn1"), (C, F, "ffn2")]:
