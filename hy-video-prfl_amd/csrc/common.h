@@ -83,7 +83,7 @@ __device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
                  (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000};
 }
 __device__ __forceinline__ void dma16_buf(i32x4 srd, uint32_t voff, uint32_t soff, uint32_t lds_dst) {
-  unsigned keep;
+  unsigned keep;     // m0 is reserved to the compiler: save / restore it around the DMA
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"

@@ -8,14 +8,19 @@
 //   B_KC: B(n,k) = B[n*ldb + k]   (nn.Linear weight [out, in] in the forward)
 //  !B_KC: B(n,k) = B[k*ldb + n]   (dX: weight read as [out][in] with k = out; dW: X [L, in])
 //
-// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16x32 tiles.
-// K-contiguous tiles live in LDS as [128 rows][64 k] (128-B rows, 16-B chunk XOR row&7) and feed
-// ds_read_b128; MN-contiguous tiles live as [64 k][128] (256-B rows, 32-B XOR swz_mn(k)) and feed
+// Two bf16 kernels, chosen by shape (launch()): every element is summed in the same k order
+// (32-deep MFMA k-steps in sequence), so their outputs are bit-identical (tested):
+//   * gemm4w_kernel (the 720p projections): 256x256 tile, 4 waves = one per SIMD, each wave
+//     128x128 with its 256 fp32 accumulators in AGPRs, operands by buffer LDS-DMA into a 4-slot
+//     ring of 32-deep K-slices (details at the kernel);
+//   * gemm_kernel (small / ragged shapes): 128x128x64 tile, 4 waves (2x2), each 64x64 = 4x4
+//     MFMA 16x16x32 tiles, register-staged double buffer, one barrier per K step.
+// K-contiguous tiles live in LDS as rows with an XOR-swizzled 16-B chunk order and feed
+// ds_read_b128; MN-contiguous tiles live as [k][128] rows (256 B, 32-B XOR swz_mn(k)) and feed
 // ds_read_b64_tr_b16 (hardware transpose), so both layouts reach the same MFMA fragment.
-// Global->LDS staging is register double-buffered: tile t+1 is loaded while tile t computes and is
-// written to the other LDS buffer after the MFMAs (one barrier per K step).
 // The MFMA is issued as D = B.A^T so each lane owns 4 consecutive n of one row m: epilogue stores
 // are 8-16 B contiguous per lane.
+// The fp8 path (C5) runs gemm256s_kernel<.., F8 = true>: 8 waves, staggered 4-phase schedule.
 #include <stdlib.h>
 
 #include "common.h"
@@ -512,12 +517,6 @@ __global__ __launch_bounds__(NT2, 1) void gemm256s_kernel(GemmArgs g) {
 // b128 lane group land on four different chunk columns).  MN-major slice image: two [32 k][128]
 // halves with 256-B rows and the swz_mn granule swizzle of the 128 kernel.
 constexpr int BK4 = 32, SLICE4 = 32768, HALF4 = 16384;
-#ifndef GEMM4W_ASM
-#define GEMM4W_ASM 1
-#endif
-#ifndef GEMM4W_SB
-#define GEMM4W_SB 1
-#endif
 
 __device__ __forceinline__ int kc_pos(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 2)) << 4); }
 
@@ -610,16 +609,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
       na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
       nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-#if GEMM4W_ASM
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][jj]) : "v"(cb[jj]), "v"(ca[i]));
-#else
-        acc[i][jj] = mfma16(cb[jj], ca[i], acc[i][jj]);
-#endif
-      }
-#if GEMM4W_SB
+      for (int jj = 0; jj < 8; ++jj)   // AGPR accumulators: the MFMA as inline asm ("+a") keeps
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"   // hipcc from switching them to
+                     : "+a"(acc[i][jj]) : "v"(cb[jj]), "v"(ca[i]));   // VGPRs and spilling
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
   };
 
@@ -659,18 +652,15 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
-  const bool fits256 = (g.K % BK) == 0 && (A_KC || g.M % BM2 == 0) && (B_KC || g.N % BN2 == 0);
-  if ((tile == 256 || tile == 4) && !fits256) return (int)hipErrorInvalidValue;
-  // the four-wave kernel addresses each operand through a 32-bit buffer offset
+  // the 256 tile needs whole 64-deep K pairs of slices and whole 256-wide MN-major extents, and
+  // addresses each operand through a 32-bit buffer offset
   const int64_t bytes_a = (A_KC ? (int64_t)g.M : (int64_t)g.K) * g.lda * 2;
   const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
-  const bool fits4w = fits256 && (g.K % 64) == 0 && g.K >= 128 && bytes_a < (1ll << 32) &&
-                      bytes_b < (1ll << 32);
-  if (tile == 4 && !fits4w) return (int)hipErrorInvalidValue;
-  if (tile == 4) {
+  const bool fits256 = (g.K % 64) == 0 && g.K >= 128 && (A_KC || g.M % BM2 == 0) &&
+                       (B_KC || g.N % BN2 == 0) && bytes_a < (1ll << 32) && bytes_b < (1ll << 32);
+  if (tile == 256 && !fits256) return (int)hipErrorInvalidValue;
+  if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
     hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
-  } else if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
-    hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
   } else {
     const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
     hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);
@@ -688,7 +678,7 @@ extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, co
                                     void* aux, int64_t ldaux, int accumulate, int tile,
                                     void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (tile != 0 && tile != 128 && tile != 256 && tile != 4) return (int)hipErrorInvalidValue;
+  if (tile != 0 && tile != 128 && tile != 256) return (int)hipErrorInvalidValue;
   // K is a contiguous extent only for K-major operands; MN-major operands take any K (row tail)
   if (K <= 0 || ((a_kmajor || b_kmajor) && (K % 8) != 0) || (N % 4) != 0)
     return (int)hipErrorInvalidValue;

@@ -1,0 +1,100 @@
+"""The reference's attention sub-modules called on their own (`diffusers_lite/wan/modules/model.py`
+WanSelfAttention `:159-200`, WanT2VCrossAttention `:205-225`, WanI2VCrossAttention `:240-271`):
+forward and input / weight gradients of the HIP composition (prfl::linear_bf16,
+prfl::flash_attention, WanRMSNorm, rope_apply) against the oracle's restatement of the same
+cast points.  Tolerances: output rel-L2 <= 1e-2, gradients <= 3e-2 (the block test's bars)."""
+import pytest
+import torch
+
+from oracle import wan_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+C, NH = 256, 2
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _module(cls, seed):
+    torch.manual_seed(seed)
+    m = cls(C, NH)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "norm" in n:
+                p.copy_(1 + 0.1 * torch.randn_like(p))
+            elif n.endswith("bias"):
+                p.copy_(0.1 * torch.randn_like(p))
+            else:
+                p.copy_(torch.randn_like(p) / C ** 0.5)
+    return m
+
+
+def _ref_proj(P, name, x):
+    return O.linear_bf16(x, P[name + ".weight"], P[name + ".bias"])
+
+
+def _check(m, out, ref, xs, xrs, tol_o=1e-2, tol_g=3e-2):
+    assert rel(out.float(), ref) < tol_o, rel(out.float(), ref)
+    up = torch.randn(out.shape, generator=torch.Generator().manual_seed(9))
+    (out.float() * up.to(DEV)).sum().backward()
+    (ref * up).sum().backward()
+    for xd, xr in zip(xs, xrs):
+        assert rel(xd.grad, xr.grad) < tol_g, rel(xd.grad, xr.grad)
+    refP = {n: p for n, p in m._ref_params.items()}
+    for n, p in m.named_parameters():
+        assert rel(p.grad, refP[n].grad) < tol_g, (n, rel(p.grad, refP[n].grad))
+
+
+def _ref_copy(m):
+    m._ref_params = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    return m._ref_params
+
+
+def test_self_attention_submodule():
+    from prfl_amd.model import WanSelfAttention
+    m = _module(WanSelfAttention, 1).to(DEV)
+    P = _ref_copy(m)
+    grid = torch.tensor([[3, 5, 7]])
+    L = 105
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(1, L, C, generator=g)
+    freqs = O.rope_freqs(C // NH)
+    xd = x.to(DEV).requires_grad_(True)
+    out = m(xd, torch.tensor([L], device=DEV), grid, freqs)
+    xr = x.clone().requires_grad_(True)
+    q = O.rms_norm(_ref_proj(P, "q", xr), P["norm_q.weight"]).view(1, L, NH, -1)
+    k = O.rms_norm(_ref_proj(P, "k", xr), P["norm_k.weight"]).view(1, L, NH, -1)
+    v = _ref_proj(P, "v", xr).view(1, L, NH, -1)
+    a = O.attention(O.rope_apply(q, grid, freqs), O.rope_apply(k, grid, freqs), v, k_len=L)
+    ref = _ref_proj(P, "o", a.flatten(2))
+    _check(m, out, ref, [xd], [xr])
+
+
+@pytest.mark.parametrize("i2v", [False, True])
+def test_cross_attention_submodules(i2v):
+    from prfl_amd.model import WanI2VCrossAttention, WanT2VCrossAttention
+    cls = WanI2VCrossAttention if i2v else WanT2VCrossAttention
+    m = _module(cls, 3 + i2v).to(DEV)
+    P = _ref_copy(m)
+    L, n_img, n_txt, klen = 105, 257 if i2v else 0, 512, 300
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(1, L, C, generator=g)
+    ctx = torch.randn(1, n_img + n_txt, C, generator=g)
+    xd, cd = x.to(DEV).requires_grad_(True), ctx.to(DEV).requires_grad_(True)
+    out = m(xd, cd, torch.tensor([klen], device=DEV))
+    xr, cr = x.clone().requires_grad_(True), ctx.clone().requires_grad_(True)
+    ci, ct = cr[:, :n_img], cr[:, n_img:]
+    q = O.rms_norm(_ref_proj(P, "q", xr), P["norm_q.weight"]).view(1, L, NH, -1)
+    k = O.rms_norm(_ref_proj(P, "k", ct), P["norm_k.weight"]).view(1, n_txt, NH, -1)
+    v = _ref_proj(P, "v", ct).view(1, n_txt, NH, -1)
+    a = O.attention(q, k, v, k_len=klen).flatten(2)
+    if i2v:
+        ki = O.rms_norm(_ref_proj(P, "k_img", ci), P["norm_k_img.weight"]).view(1, n_img, NH, -1)
+        vi = _ref_proj(P, "v_img", ci).view(1, n_img, NH, -1)
+        a = a + O.attention(q, ki, vi).flatten(2)
+    ref = _ref_proj(P, "o", a)
+    _check(m, out, ref, [xd, cd], [xr, cr])

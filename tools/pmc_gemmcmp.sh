@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC comparison of prfl_gemm and hipBLASLt on the QKV forward shape (prof_kernels.py gemmcmp):
 # one counter group per rocprofv3 run, each under its own time limit.
-out=$GRAFT_REPO_ROOT/gpurun_out/pmc_gemmcmp
+out=$GRAFT_REPO_ROOT/gpurun_out/pmc_gemmcmp${PRFL_GEMM_TILE:+_t$PRFL_GEMM_TILE}
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 export PRFL_PROF_L=73920

@@ -88,8 +88,9 @@ elif which == "gemmcmp":
     x = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(3 * C, C, device=dev, generator=g) * 0.02).to(torch.bfloat16)
     y = torch.empty(L, 3 * C, device=dev, dtype=torch.bfloat16)
+    tile = int(os.environ.get("PRFL_GEMM_TILE", 0))
     for i in range(reps):
-        ops.linear(x, w, out=y)
+        ops.linear(x, w, out=y, tile=tile)
         torch.matmul(x, w.t(), out=y)
     torch.cuda.synchronize()
     print("gemmcmp done", flush=True)
