@@ -8,11 +8,13 @@
 //   B_KC: B(n,k) = B[n*ldb + k]   (nn.Linear weight [out, in] in the forward)
 //  !B_KC: B(n,k) = B[k*ldb + n]   (dX: weight read as [out][in] with k = out; dW: X [L, in])
 //
-// Two bf16 kernels, chosen by shape (launch()): every element is summed in the same k order
-// (32-deep MFMA k-steps in sequence), so their outputs are bit-identical (tested):
-//   * gemm4w_kernel (the 720p projections): 256x256 tile, 4 waves = one per SIMD, each wave
-//     128x128 with its 256 fp32 accumulators in AGPRs, operands by buffer LDS-DMA into a 4-slot
-//     ring of 32-deep K-slices (details at the kernel);
+// Three bf16 kernels, chosen by shape and epilogue (launch()): every element is summed in the
+// same k order (32-deep MFMA k-steps in sequence), so their outputs are bit-identical (tested):
+//   * gemm4w_kernel (the 720p projections: plain bf16, fp32 / accumulate, dGELU): 256x256 tile,
+//     4 waves = one per SIMD, each wave 128x128 with its 256 fp32 accumulators in AGPRs,
+//     operands by buffer LDS-DMA into a 4-slot ring of 32-deep K-slices (details at the kernel);
+//   * gemm256s_kernel (the 720p projections with the GELU or gated-residual epilogue): 256x256
+//     tile, 8 waves, staggered 4-phase LDS-DMA schedule (details at the kernel);
 //   * gemm_kernel (small / ragged shapes): 128x128x64 tile, 4 waves (2x2), each 64x64 = 4x4
 //     MFMA 16x16x32 tiles, register-staged double buffer, one barrier per K step.
 // K-contiguous tiles live in LDS as rows with an XOR-swizzled 16-B chunk order and feed
@@ -20,7 +22,7 @@
 // ds_read_b64_tr_b16 (hardware transpose), so both layouts reach the same MFMA fragment.
 // The MFMA is issued as D = B.A^T so each lane owns 4 consecutive n of one row m: epilogue stores
 // are 8-16 B contiguous per lane.
-// The fp8 path (C5) runs gemm256s_kernel<.., F8 = true>: 8 waves, staggered 4-phase schedule.
+// The fp8 path (C5) runs gemm256s_kernel<.., F8 = true>.
 #include <stdlib.h>
 
 #include "common.h"
@@ -541,6 +543,109 @@ __device__ __forceinline__ bf16x8 read_frag4(const char* lds, int base, int lane
   return read_frag<false>(lds + (base >> 7) * 8192, base & 127, 0, lane);
 }
 
+// Epilogue of the four-wave kernel: lane owns rows mb + 16 i (i < 8) and columns nb + 16 j + r
+// (j < 8, r < 4).  With one wave per SIMD nothing hides a load's latency, so (1) the per-column
+// bias / gate values are loaded once per lane (not once per row block), and (2) the per-element
+// inputs (fp32 / bf16 residual, fp32 accumulator, dGELU pre-activation) of row block i+1 are
+// loaded before row block i is computed and stored.  The in-place residual (res == C) stays
+// correct: a row block is read before anything of it is written.  Same arithmetic, in the same
+// order, as epilogue_tile (outputs bit-identical to the 128 kernel).
+template <int EPI>
+__device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)[8][8], int mb, int nb) {
+  constexpr bool HAS_IN = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_DGELU;
+  float bias[8][4], gate[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = nb + 16 * j;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bias[j][r] = (EPI != EPI_F32 && EPI != EPI_DGELU && g.bias && n < g.N) ? bf2f(g.bias[n + r]) : 0.f;
+      gate[j][r] = (EPI == EPI_RESID && g.gate && n < g.N) ? g.gate[n + r] : 1.f;
+    }
+  }
+  auto load_in = [&](int i, f32x4 (&in)[8]) {
+    const int m = mb + 16 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nb + 16 * j;
+      in[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (m >= g.M || n >= g.N) continue;
+      if (EPI == EPI_F32) {
+        if (g.accumulate) in[j] = *(const f32x4*)((const float*)g.C + (int64_t)m * g.ldc + n);
+      } else if (EPI == EPI_DGELU) {
+        const bf16x4 pre = *(const bf16x4*)(g.aux + (int64_t)m * g.ldaux + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) in[j][r] = bf2f(pre[r]);
+      } else if (EPI == EPI_RESID) {
+        if (g.res_bf16) {
+          const bf16x4 rr = *(const bf16x4*)((const bf16*)g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) in[j][r] = bf2f(rr[r]);
+        } else {
+          in[j] = *(const f32x4*)((const float*)g.res + (int64_t)m * g.ldr + n);
+        }
+      }
+    }
+  };
+  f32x4 cur[8], nxt[8];
+  if (HAS_IN) load_in(0, cur);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (HAS_IN && i + 1 < 8) load_in(i + 1, nxt);
+    const int m = mb + 16 * i;
+    if (m < g.M) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = nb + 16 * j;
+        if (n >= g.N) continue;
+        const f32x4 v = acc[i][j];
+        if (EPI == EPI_F32) {
+          *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + cur[j] : v;
+        } else if (EPI == EPI_DGELU) {
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(cur[j][r]));
+          *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+        } else {
+          float y[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bias[j][r]);
+          if (EPI == EPI_BF16) {
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
+            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+          } else if (EPI == EPI_GELU) {
+            bf16x4 o, pre;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              pre[r] = f2bf(y[r]);
+              o[r] = f2bf(gelu_tanh(y[r]));
+            }
+            if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
+            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+          } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
+            if (g.aux) {
+              bf16x4 yo;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
+              *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
+            }
+            f32x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = cur[j][r] + mul_rn(y[r], gate[j][r]);
+            *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
+          }
+        }
+      }
+    }
+    if (HAS_IN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+    }
+  }
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
@@ -633,17 +738,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // the MFMAs are inline asm: the compiler does not see their AGPR writes, so pad the
   // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
-      if (n >= g.N) continue;
-      epilogue_tile<A_KC, B_KC, EPI>(g, acc[i][j], m, n);
-    }
-  }
+  epilogue4w<EPI>(g, acc, m0 + wm * 128 + (lane & 15), n0 + wn * 128 + 4 * (lane >> 4));
 }
 
 // tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced
@@ -652,15 +747,23 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
-  // the 256 tile needs whole 64-deep K pairs of slices and whole 256-wide MN-major extents, and
-  // addresses each operand through a 32-bit buffer offset
-  const int64_t bytes_a = (A_KC ? (int64_t)g.M : (int64_t)g.K) * g.lda * 2;
-  const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
-  const bool fits256 = (g.K % 64) == 0 && g.K >= 128 && (A_KC || g.M % BM2 == 0) &&
-                       (B_KC || g.N % BN2 == 0) && bytes_a < (1ll << 32) && bytes_b < (1ll << 32);
+  // the 256 tiles need whole 64-deep K steps and whole 256-wide MN-major extents
+  const bool fits256 = (g.K % BK) == 0 && g.K >= 128 && (A_KC || g.M % BM2 == 0) &&
+                       (B_KC || g.N % BN2 == 0);
   if (tile == 256 && !fits256) return (int)hipErrorInvalidValue;
   if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
-    hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
+    // GELU / gated-residual epilogues: the 8-wave kernel (its two waves per SIMD overlap the
+    // VALU-heavy tanh and the residual round trip; the four-wave kernel is 6 % / 1-3 % slower
+    // there, profiles/r02_gemm_4w_epilogues.txt).  Everything else: the four-wave kernel, which
+    // addresses each operand through a 32-bit buffer offset.
+    const int64_t bytes_a = (A_KC ? (int64_t)g.M : (int64_t)g.K) * g.lda * 2;
+    const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
+    const bool four = EPI != EPI_GELU && EPI != EPI_RESID && bytes_a < (1ll << 32) &&
+                      bytes_b < (1ll << 32);
+    if (four)
+      hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
   } else {
     const int ntm = (g.M + BM - 1) / BM, ntn = (g.N + BN - 1) / BN;
     hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI>), dim3(ntm * ntn), dim3(NT), 0, s, g);

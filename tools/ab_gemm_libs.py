@@ -25,8 +25,12 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--shapes", default="qkv,o,ffn1,ffn2")
+    ap.add_argument("--passes", default="fwd,dx,dw")
+    ap.add_argument("--tiles", default=None, help="per-lib tile codes, comma separated")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
+    tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else [a.tile] * len(libs)
+    tile_of = {id(lib): t for lib, t in zip(libs, tiles)}
     L, C, F = 73920, 5120, 13824
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -47,12 +51,35 @@ def main():
                 args = (x.data_ptr(), K, 1, w.data_ptr(), K, 1, o.data_ptr(), N, L, N, K, 0)
             elif pas == "dx":  # dx[L,K] = dy[L,N] w[N,K]
                 args = (dy.data_ptr(), N, 1, w.data_ptr(), K, 0, o.data_ptr(), K, L, K, N, 0)
+            elif pas == "gelu":   # FFN-up: GELU epilogue, pre-activation to aux
+                rc = lib.prfl_gemm_bf16_tiled(x.data_ptr(), K, 1, w.data_ptr(), K, 1, o.data_ptr(), N, L, N, K, 1,
+                                              None, None, None, 0, 0, aux.data_ptr(), N, 0, tile_of[id(lib)], st)
+                assert rc == 0, rc
+                return
+            elif pas == "resid":  # o-proj / FFN-down: x + bf16(y) * gate (fp32), y to aux
+                rc = lib.prfl_gemm_bf16_tiled(x.data_ptr(), K, 1, w.data_ptr(), K, 1, o.data_ptr(), N, L, N, K, 2,
+                                              None, gate.data_ptr(), res.data_ptr(), N, 0, aux.data_ptr(), N, 0,
+                                              tile_of[id(lib)], st)
+                assert rc == 0, rc
+                return
+            elif pas == "dwacc":  # weight grad accumulated into fp32 .grad
+                rc = lib.prfl_gemm_bf16_tiled(dy.data_ptr(), N, 0, x.data_ptr(), K, 0, o.data_ptr(), K, N, K, L, 3,
+                                              None, None, None, 0, 0, None, 0, 1, tile_of[id(lib)], st)
+                assert rc == 0, rc
+                return
             else:              # dw[N,K] = dy^T x (fp32)
                 args = (dy.data_ptr(), N, 0, x.data_ptr(), K, 0, o.data_ptr(), K, N, K, L, 3)
-            rc = lib.prfl_gemm_bf16_tiled(*args, None, None, None, 0, 0, None, 0, 0, a.tile, st)
+            rc = lib.prfl_gemm_bf16_tiled(*args, None, None, None, 0, 0, None, 0, 0, tile_of[id(lib)], st)
             assert rc == 0, rc
 
-        for pas in ("fwd", "dx", "dw"):
+        gate = torch.randn(N, device=dev, generator=g)
+        res = torch.randn(L, N, device=dev, generator=g)
+        aux = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+        for o in outs:
+            o["gelu"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+            o["resid"] = torch.empty(L, N, device=dev)
+            o["dwacc"] = torch.zeros(N, K, device=dev)
+        for pas in a.passes.split(","):
             ts = [[] for _ in libs]
             for r in range(a.reps + 1):
                 for i, lib in enumerate(libs):
@@ -63,7 +90,7 @@ def main():
                     torch.cuda.synchronize()
                     if r:
                         ts[i].append(e0.elapsed_time(e1))
-            same = all(torch.equal(outs[0][pas], o[pas]) for o in outs[1:])
+            same = all(torch.equal(outs[0][pas], o[pas]) for o in outs[1:]) if pas != "dwacc" else "n/a"
             meds = [statistics.median(t) for t in ts]
             print(f"{name:5s} {pas:3s}: " + " | ".join(f"lib{i} {m:6.2f} ms {fl / m / 1e9:5.0f} TF/s"
                                                        for i, m in enumerate(meds))
