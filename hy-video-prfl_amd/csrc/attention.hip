@@ -133,6 +133,9 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // SCHED > 0 interleaves the LDS reads SCHED+1 MFMAs ahead of their use (sched_group_barrier).
 // SHORT_KV: separate instantiation for the 512/257-key cross-attention (SCHED 1) so profiles
 // separate it from the self-attention (SCHED 2).
+#ifndef ATTN_FWD_SCHED
+#define ATTN_FWD_SCHED 2
+#endif
 template <bool SHORT_KV, int SCHED, int NKT>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
@@ -644,7 +647,7 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
   prfl_prof::begin(kid, s);
   const dim3 grid((unsigned)(((Lq + 255) / 256) * H * B));
   if (kid == KID_ATTN_FWD)
-    hipLaunchKernelGGL((attn_fwd_kernel<false, 2, 3>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3>), grid, dim3(512), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);

@@ -1,0 +1,64 @@
+"""Dev A/B of N builds of the attention kernels in ONE process, interleaved (guide §5.4 rule 24):
+    python tools/ab_attn_libs.py <lib1.so> <lib2.so> ... [--L 73920] [--reps 6] [--bwd]
+prfl_attn_fwd (and with --bwd prfl_attn_bwd) at L tokens, 40 heads, HIP events on the launch
+stream; prints per-build medians and whether all builds' outputs are bit-identical."""
+import argparse
+import statistics
+
+import torch
+
+from ab_attn import load
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--L", type=int, default=73920)
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--bwd", action="store_true")
+    a = ap.parse_args()
+    libs = [load(p) for p in a.libs]
+    L, H, C = a.L, 40, 5120
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    qkv = torch.randn(L, 3 * C, generator=g, device=dev).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    do = torch.randn(L, C, generator=g, device=dev).to(torch.bfloat16)
+    outs = [dict(o=torch.empty(L, C, dtype=torch.bfloat16, device=dev), lse=torch.empty(H, L, device=dev),
+                 delta=torch.empty(H, L, device=dev), dq=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
+                 dk=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
+                 dv=torch.empty(L, C, dtype=torch.bfloat16, device=dev)) for _ in libs]
+    sc = 128 ** -0.5
+    st = torch.cuda.current_stream().cuda_stream
+
+    def fwd(lib, b):
+        assert lib.prfl_attn_fwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                                 b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc, st) == 0
+
+    def bwd(lib, b):
+        assert lib.prfl_attn_bwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                                 b["o"].data_ptr(), C, 0, do.data_ptr(), C, 0, b["lse"].data_ptr(),
+                                 b["delta"].data_ptr(), b["dq"].data_ptr(), C, 0, b["dk"].data_ptr(), C, 0,
+                                 b["dv"].data_ptr(), C, 0, 1, L, L, H, L, sc, st) == 0
+
+    work = [("fwd", fwd, 4 * L * L * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
+    for w, fn, fl in work:
+        ts = [[] for _ in libs]
+        for r in range(a.reps + 1):
+            for i, lib in enumerate(libs):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(lib, outs[i])
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    ts[i].append(e0.elapsed_time(e1))
+        meds = [statistics.median(t) for t in ts]
+        keys = ("o", "lse") if w == "fwd" else ("dq", "dk", "dv")
+        same = all(torch.equal(outs[0][n], o[n]) for o in outs[1:] for n in keys)
+        print(f"{w}: " + " | ".join(f"lib{i} {m:.2f} ms {fl / m / 1e9:.0f} TF/s" for i, m in enumerate(meds))
+              + f" | identical {same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
