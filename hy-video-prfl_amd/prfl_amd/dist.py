@@ -26,15 +26,19 @@ def is_dist():
 
 
 class GradReducer:
-    def __init__(self, params, small_numel=1 << 16):
+    def __init__(self, params, small_numel=1 << 16, min_world=2):
+        # min_world=1 hooks a one-rank process group too (exercises the exchange end to end on
+        # a single device: the RCCL AVG over one rank is exact)
         self.params = [p for p in params if p.requires_grad]
-        self.world = dist.get_world_size() if is_dist() else 1
+        on = dist.is_available() and dist.is_initialized() and dist.get_world_size() >= min_world
+        self.world = dist.get_world_size() if on else 1
+        self.active = on
         self.small_numel = small_numel
         self.works = []
         self.small_pending = []
-        self.backend = dist.get_backend() if is_dist() else None
+        self.backend = dist.get_backend() if on else None
         self.handles = []
-        if self.world > 1:
+        if on:
             for p in self.params:
                 self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
@@ -63,7 +67,7 @@ class GradReducer:
 
     def end(self):
         """Call after loss.backward(): completes the exchange."""
-        if self.world > 1:
+        if self.active:
             self._flush_small()
             for w, payload in self.works:
                 w.wait()
