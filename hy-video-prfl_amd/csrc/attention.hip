@@ -406,22 +406,35 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     const int kk = min(k0 + row, a.Lk - 1);
     dma16(Vb + (int64_t)kk * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
   }
-  // Q / dO tile (offB image, row and transposed reads): 16 + 16 pieces, 4 per wave; LSE, D rows
+  // Q / dO tile (offB image, row and transposed reads): 16 + 16 pieces, 4 per wave; LSE, D rows.
+  // Through buffer resources rebased per tile: the per-lane offsets are loop-invariant 32-bit
+  // VGPRs (64-bit per-lane pointers spilled at 256 VGPRs and serialised every tile's DMA issue
+  // behind scratch reloads); rows past Lq land as zeros (the tail mask zeroes their P / dS).
+  uint32_t voq[2], vod[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (w * 2 + i) * 4 + (lane >> 4), pc = lane & 15;
+    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+    voq[i] = (uint32_t)(row * a.ldq * 2) + ((pc ^ swzb) << 4);
+    vod[i] = (uint32_t)(row * a.lddo * 2) + ((pc ^ swzb) << 4);
+  }
   auto dma_tile = [&](int t, int st) {
     char* Qs = smem + V_BYTES + st * STAGE;
     char* Ds = Qs + 16384;
-    const int qb = t * 64;
+    const int qb = t * 64, rows = min(a.Lq - qb, 64);   // the record range stays < 2^32 bytes
+    const i32x4 sq = make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2));
+    const i32x4 sd = make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2));
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int piece = w * 2 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-      const int q = min(qb + row, a.Lq - 1);
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16(Qb + (int64_t)q * a.ldq + ((pc ^ swzb) << 3), lds_addr(Qs + piece * 1024));
-      dma16(dOb + (int64_t)q * a.lddo + ((pc ^ swzb) << 3), lds_addr(Ds + piece * 1024));
+      dma16_buf(sq, voq[i], 0, lds_addr(Qs + (w * 2 + i) * 1024));
+      dma16_buf(sd, vod[i], 0, lds_addr(Ds + (w * 2 + i) * 1024));
     }
-    if (w < 2) {
-      const int q = min(qb + lane, a.Lq - 1);
-      dma4((w == 0 ? lseb : delb) + q, lds_addr(Qs + 32768 + w * 256));
+    if (w < 2) {   // lane * 4 re-derived here (volatile: not hoisted into a register kept live)
+      uint32_t l4;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
+                   "v_lshlrev_b32 %0, 2, %0" : "=v"(l4));
+      dma4_buf(make_srd((w == 0 ? lseb : delb) + qb, (uint32_t)(rows * 4)), l4,
+               lds_addr(Qs + 32768 + w * 256));
     }
   };
   f32x16 dk[4], dv[4];
@@ -462,10 +475,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = kvalid ? __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]) : 0.f;
-          if (tail && qb + q4 + r >= a.Lq) p = 0.f;
+          const float p = __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]);
           sacc[rg * 4 + r] = p;
           dpt[rg * 4 + r] = p * (dpt[rg * 4 + r] - d4[r]);
+        }
+        if (__builtin_expect(tail, 0)) {   // rows past Lq: P = dS = 0 (last tile only)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (qb + q4 + r >= a.Lq) { sacc[rg * 4 + r] = 0.f; dpt[rg * 4 + r] = 0.f; }
         }
       }
       bf16x8 pk[2], dk8[2];
@@ -506,8 +523,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         bf16x4 vk, vv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          vk[r] = f2bf(dk[dt][rg * 4 + r] * a.scale);
-          vv[r] = f2bf(dv[dt][rg * 4 + r]);
+          vk[r] = f2bf(kvalid ? dk[dt][rg * 4 + r] * a.scale : 0.f);
+          vv[r] = f2bf(kvalid ? dv[dt][rg * 4 + r] : 0.f);
         }
         *(bf16x4*)(dKb + dt * 32 + 8 * rg + 4 * hh) = vk;
         *(bf16x4*)(dVb + dt * 32 + 8 * rg + 4 * hh) = vv;
@@ -547,17 +564,27 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
   const int nkv = (a.k_len + TK - 1) / TK;
-  // K / V tile by LDS-DMA: 16 + 16 pieces of 4 rows, 2 + 2 per wave, swizzles on the source
+  // K / V tile by LDS-DMA: NKT * 8 + NKT * 8 pieces of 4 rows, NKT + NKT per wave, swizzles on
+  // the source; buffer resources rebased per tile keep the per-lane offsets 32-bit and loop
+  // invariant, rows past Lk land as zeros (masked: they are past k_len)
+  uint32_t vok[NKT], vov[NKT];
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) {
+    const int row = (w * NKT + i) * 4 + (lane >> 4), pc = lane & 15;
+    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+    vok[i] = (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4);
+    vov[i] = (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4);
+  }
   auto dma = [&](int t, int st) {
     char* Ks = smem + st * SB;
     char* Vs = Ks + SV;
+    const int rows = min(a.Lk - t * TK, TK);
+    const i32x4 sk = make_srd(Kb + (int64_t)t * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
+    const i32x4 sv = make_srd(Vb + (int64_t)t * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
 #pragma unroll
     for (int i = 0; i < NKT; ++i) {
-      const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-      const int kr = min(t * TK + row, a.Lk - 1);
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16(Kb + (int64_t)kr * a.ldk + ((pc ^ swzb) << 3), lds_addr(Ks + piece * 1024));
-      dma16(Vb + (int64_t)kr * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
+      dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
+      dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
   dma(0, 0);
@@ -583,9 +610,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float p = key < a.k_len ? __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse) : 0.f;
+        const float p = __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
         dpt[r] = p * (dpt[r] - del);
+      }
+      if (__builtin_expect(kb + kt * 32 + 32 > a.k_len, 0)) {   // keys >= k_len: dS = 0
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) dpt[r] = 0.f;
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)

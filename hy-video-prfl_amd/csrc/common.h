@@ -2,10 +2,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -90,6 +92,18 @@ __device__ __forceinline__ void dma16_buf(i32x4 srd, uint32_t voff, uint32_t sof
       : "=&s"(keep)
       : "v"(voff), "s"(srd), "s"(__builtin_amdgcn_readfirstlane(lds_dst)),
         "s"(__builtin_amdgcn_readfirstlane(soff))
+      : "memory");
+}
+
+// 4-B-per-lane buffer variant (buffer_load_dword ... lds): lane i lands at lds_dst + 4 i; a lane
+// whose offset is past the SRD's num_records lands 0.
+__device__ __forceinline__ void dma4_buf(i32x4 srd, uint32_t voff, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
       : "memory");
 }
 
