@@ -89,8 +89,11 @@ class WanLayerNorm(nn.LayerNorm):
 
 
 class _Attn(nn.Module):
-    """Parameter container with the reference attention layout (`model.py:138-271`).  Its math
-    runs fused inside WanAttentionBlock (prfl_amd/block.py)."""
+    """The reference attention modules (`model.py:138-271`): same parameters and forward
+    signatures.  Inside a WanAttentionBlock their math runs fused (prfl_amd/block.py, one
+    `prfl::wan_block` op per block); called on their own they compose the custom ops with the
+    reference's cast points: `prfl::linear_bf16` projections (autocast bf16 Linear), WanRMSNorm
+    (fp32, rounded to bf16, x fp32 weight), rope_apply (fp64) and `prfl::flash_attention`."""
 
     def __init__(self, dim, num_heads, window_size=(-1, -1), qk_norm=True, eps=1e-6, img=False):
         super().__init__()
@@ -105,21 +108,52 @@ class _Attn(nn.Module):
             self.v_img = nn.Linear(dim, dim)
             self.norm_k_img = WanRMSNorm(dim, eps=eps) if qk_norm else nn.Identity()
 
-    def forward(self, *a, **k):
-        raise RuntimeError("attention sub-modules run fused inside WanAttentionBlock.forward")
+    def _proj(self, name, x):
+        lin = getattr(self, name)
+        return linear_bf16(x, lin.weight, lin.bias)
+
+    def _heads(self, t):
+        return t.view(t.shape[0], -1, self.num_heads, self.head_dim)
+
+    def _kv(self, ctx, k="k", v="v", nk="norm_k"):
+        return self._heads(getattr(self, nk)(self._proj(k, ctx))), self._heads(self._proj(v, ctx))
+
+    def _qkv(self, x, ctx):
+        return (self._heads(self.norm_q(self._proj("q", x))),) + self._kv(ctx)
 
 
 class WanSelfAttention(_Attn):
-    pass
+    def forward(self, x, seq_lens, grid_sizes, freqs):
+        """model.py:163-201 (no sequence parallelism: DP replaces SP)."""
+        from .attention import flash_attention
+        q, k, v = self._qkv(x, x)
+        q, k = rope_apply(q, grid_sizes, freqs), rope_apply(k, grid_sizes, freqs)
+        a = flash_attention(q, k, v, k_lens=seq_lens, window_size=self.window_size)
+        return self._proj("o", a.flatten(2))
 
 
 class WanT2VCrossAttention(_Attn):
-    pass
+    def forward(self, x, context, context_lens):
+        """model.py:206-226."""
+        from .attention import flash_attention
+        q, k, v = self._qkv(x, context)
+        return self._proj("o", flash_attention(q, k, v, k_lens=context_lens).flatten(2))
 
 
 class WanI2VCrossAttention(_Attn):
     def __init__(self, dim, num_heads, window_size=(-1, -1), qk_norm=True, eps=1e-6):
         super().__init__(dim, num_heads, window_size, qk_norm, eps, img=True)
+
+    def forward(self, x, context, context_lens):
+        """model.py:244-271: the leading context tokens are the image (CLIP) tokens."""
+        from .attention import flash_attention
+        n_img = context.shape[1] - T5_CONTEXT_TOKEN_NUMBER
+        ctx_img, ctx = context[:, :n_img], context[:, n_img:]
+        q, k, v = self._qkv(x, ctx)
+        ki, vi = self._kv(ctx_img, "k_img", "v_img", "norm_k_img")
+        img_x = flash_attention(q, ki, vi, k_lens=None)
+        out = flash_attention(q, k, v, k_lens=context_lens)
+        return self._proj("o", out.flatten(2) + img_x.flatten(2))
 
 
 WAN_CROSSATTENTION_CLASSES = {"t2v_cross_attn": WanT2VCrossAttention,

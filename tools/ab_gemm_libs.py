@@ -62,6 +62,12 @@ def main():
                                               tile_of[id(lib)], st)
                 assert rc == 0, rc
                 return
+            elif pas == "dgelu":  # FFN-up backward: dX through the GELU derivative of aux
+                rc = lib.prfl_gemm_bf16_tiled(dy.data_ptr(), N, 1, w.data_ptr(), K, 0, o.data_ptr(), K, L, K, N, 4,
+                                              None, None, None, 0, 0, pre_k.data_ptr(), K, 0,
+                                              tile_of[id(lib)], st)
+                assert rc == 0, rc
+                return
             elif pas == "dwacc":  # weight grad accumulated into fp32 .grad
                 rc = lib.prfl_gemm_bf16_tiled(dy.data_ptr(), N, 0, x.data_ptr(), K, 0, o.data_ptr(), K, N, K, L, 3,
                                               None, None, None, 0, 0, None, 0, 1, tile_of[id(lib)], st)
@@ -75,7 +81,9 @@ def main():
         gate = torch.randn(N, device=dev, generator=g)
         res = torch.randn(L, N, device=dev, generator=g)
         aux = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+        pre_k = torch.randn(L, K, device=dev, generator=g).to(torch.bfloat16)
         for o in outs:
+            o["dgelu"] = torch.empty(L, K, device=dev, dtype=torch.bfloat16)
             o["gelu"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
             o["resid"] = torch.empty(L, N, device=dev)
             o["dwacc"] = torch.zeros(N, K, device=dev)
