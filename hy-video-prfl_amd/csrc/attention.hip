@@ -18,6 +18,8 @@
 //   attn_bwd_dq_kernel    dQ: 8 waves x 32 queries, 96-key K/V tiles streamed
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -33,6 +35,11 @@ struct AttnArgs {
   int Lq, Lk, H, k_len;
   float sl2;             // softmax_scale * log2(e)
   int B;
+  // split-KV tail (see prfl_attn_fwd): workgroups >= nmain each take 1/split of the key tiles
+  // of one of the last (sample, head, query tile) units; partials go to Opart / MLpart
+  int nmain, split;
+  float* Opart;          // [tail wg][256 q][128 d] unnormalised O (fp32)
+  float* MLpart;         // [tail wg][256 q][2] (row max, row sum), log2 domain
 };
 
 struct AttnBwdArgs {
@@ -96,8 +103,7 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
 // per launch (FETCH_SIZE x 2), time 98.59 -> 98.34 ms (unchanged: the kernel is not memory
 // bound); the same grouping made dK/dV + dQ 2.3 % SLOWER, so the backward kernels keep the plain
 // (tile, head, sample) grid.
-__device__ __forceinline__ void xcd_tile(int ntile, int nbh, int& bh, int& tile) {
-  const int bid = blockIdx.x;
+__device__ __forceinline__ void xcd_tile(int ntile, int nbh, int& bh, int& tile, int bid) {
   if ((nbh & 7) == 0) {
     const int i = bid >> 3, per = nbh >> 3;
     bh = (bid & 7) * per + i / ntile;
@@ -128,8 +134,8 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // and waves 4-7 run one barrier behind waves 0-3 at s_setprio 1 (the younger half; guide item
 // 4), so on each SIMD one wave's X overlaps its partner's Y.  Tile T is issued by waves 0-3 in
 // X_{T-1} / by waves 4-7 in Y_{T-2} into the stage tile T-3 left, and retired by each issuing
-// wave's vmcnt(0) before the barrier that ends that phase.  LDS addresses and DMA sources are
-// per-lane constants hoisted out of the loop (the key clamp is only needed on the last tile).
+// wave's vmcnt(0) before the barrier that ends that phase.  LDS addresses and DMA source offsets
+// are per-lane 32-bit constants hoisted out of the loop (buffer resources rebased per tile).
 // SCHED > 0 interleaves the LDS reads SCHED+1 MFMAs ahead of their use (sched_group_barrier).
 // SHORT_KV: separate instantiation for the 512/257-key cross-attention (SCHED 1) so profiles
 // separate it from the self-attention (SCHED 2).
@@ -142,8 +148,14 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
   constexpr int SB = 2 * SV;                   // bytes of one [K | V] ring stage
   __shared__ __attribute__((aligned(16))) char smem[3 * SB];   // ring of [K | V] tiles
+  // unit = (sample, head, query tile); the last units of the grid are split over `split`
+  // workgroups that each take a contiguous share of the key tiles (the final dispatch round
+  // would otherwise run a handful of workgroups on an otherwise idle chip)
+  const int bid = blockIdx.x;
+  const bool part = bid >= a.nmain;
+  const int unit = part ? a.nmain + (bid - a.nmain) / a.split : bid;
   int bh, tile;
-  xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile);
+  xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile, unit);
   const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,7 +179,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float m = NEG_INF, lsum = 0.f;
-  const int nkv = (a.k_len + TK - 1) / TK;
+  // key tiles [t0, t0 + nkv) of this workgroup
+  int t0 = 0, nkv = (a.k_len + TK - 1) / TK;
+  if (part) {
+    const int per = (nkv + a.split - 1) / a.split, s = (bid - a.nmain) % a.split;
+    t0 = min(s * per, nkv);
+    nkv = min(nkv, t0 + per) - t0;
+  }
 
   // hoisted LDS read offsets (bytes within a [K | V] stage)
   int koff[8];
@@ -180,39 +198,29 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     voff[dt] = SV + offB(4 * (g >> 1) + qq, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
     voff8[dt] = SV + offB(4 * (g >> 1) + qq + 8, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
   }
-  // hoisted DMA source offsets (elements) of this lane's two K and two V 16-B chunks
-  int64_t ksrc[NKT], vsrc[NKT];
-  int drow[NKT];
+  // K / V tile DMA through buffer resources rebased per tile (SALU only): the per-lane byte
+  // offsets are loop-invariant 32-bit VGPRs, so the loop carries no 64-bit per-lane address
+  // arithmetic; rows past Lk are out of the resource's range and land as zeros (keys >= k_len:
+  // masked to -inf, so the result is that of the clamped-row form, bit for bit)
+  uint32_t vok[NKT], vov[NKT];
 #pragma unroll
   for (int i = 0; i < NKT; ++i) {
-    const int piece = w * NKT + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+    const int row = (w * NKT + i) * 4 + (lane >> 4), pc = lane & 15;
     const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-    drow[i] = row;
-    ksrc[i] = (int64_t)row * a.ldk + ((pc ^ (row & 15)) << 3);
-    vsrc[i] = (int64_t)row * a.ldv + ((pc ^ swzb) << 3);
+    vok[i] = (uint32_t)(row * a.ldk * 2) + ((pc ^ (row & 15)) << 4);
+    vov[i] = (uint32_t)(row * a.ldv * 2) + ((pc ^ swzb) << 4);
   }
-  const bool clamp_last = (int64_t)nkv * TK > a.Lk;
-  auto dma = [&](int t, int st) {
+  auto dma = [&](int t, int st) {      // local tile t = key tile t0 + t
     char* Ks = smem + st * SB;
     char* Vs = Ks + SV;
-    if (clamp_last && t == nkv - 1) {
+    const int tg = t0 + t;
+    const int rows = min(a.Lk - tg * TK, TK);
+    const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
+    const i32x4 sv = make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
 #pragma unroll
-      for (int i = 0; i < NKT; ++i) {
-        const int piece = w * NKT + i, row = drow[i], pc = lane & 15;
-        const int key = min(t * TK + row, a.Lk - 1);
-        const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-        dma16(Kb + (int64_t)key * a.ldk + ((pc ^ (row & 15)) << 3), lds_addr(Ks + piece * 1024));
-        dma16(Vb + (int64_t)key * a.ldv + ((pc ^ swzb) << 3), lds_addr(Vs + piece * 1024));
-      }
-    } else {
-      const bf16* kt0 = Kb + (int64_t)t * TK * a.ldk;
-      const bf16* vt0 = Vb + (int64_t)t * TK * a.ldv;
-#pragma unroll
-      for (int i = 0; i < NKT; ++i) {
-        const int piece = w * NKT + i;
-        dma16(kt0 + ksrc[i], lds_addr(Ks + piece * 1024));
-        dma16(vt0 + vsrc[i], lds_addr(Vs + piece * 1024));
-      }
+    for (int i = 0; i < NKT; ++i) {
+      dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
+      dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
   auto bar = [&]() {
@@ -221,7 +229,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     asm volatile("" ::: "memory");
   };
 
-  dma(0, 0);
+  if (nkv > 0) dma(0, 0);
   if (nkv > 1) dma(1, 1);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
   bar();
@@ -283,7 +291,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     // ---------------- Y_t ----------------
     if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
     if (t < nkv) {
-      const int kbase = t * TK;
+      const int kbase = (t0 + t) * TK;
       if (kbase + TK > a.k_len) {
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
@@ -329,7 +337,17 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   if (gp == 0) bar();
   lsum += __shfl_xor(lsum, 32, 64);
   const int qr = q0 + w * 32 + l32;
-  if (qr < a.Lq) {
+  if (part) {            // unnormalised partial (O, m, l) of this key share, merged by attn_merge
+    const int j = bid - a.nmain, row = w * 32 + l32;
+    float* Op = a.Opart + ((int64_t)j * 256 + row) * HD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+        *(f32x4*)(Op + dt * 32 + 8 * rg + 4 * hh) =
+            (f32x4){o[dt][rg * 4], o[dt][rg * 4 + 1], o[dt][rg * 4 + 2], o[dt][rg * 4 + 3]};
+    if (hh == 0) *(f32x2*)(a.MLpart + ((int64_t)j * 256 + row) * 2) = (f32x2){m, lsum};
+  } else if (qr < a.Lq) {
     bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
     const float inv = 1.f / lsum;
 #pragma unroll
@@ -655,36 +673,125 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
 }
 
+// Merge of the split-KV tail partials: one workgroup per split unit, 8 query rows per pass (32
+// lanes x 4 columns per row): m = max_s m_s, l = sum_s l_s 2^(m_s - m), O = sum_s O_s 2^(m_s - m)
+// / l, lse2 = m + log2(l) -- the flash-decoding combination of the per-share online softmax.
+__global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
+  const int unit = a.nmain + blockIdx.x;
+  int bh, tile;
+  xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile, unit);
+  const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
+  const int c = (threadIdx.x & 31) * 4;
+  const int j0 = blockIdx.x * a.split;
+  for (int row = threadIdx.x >> 5; row < 256; row += 8) {
+    const int qr = q0 + row;
+    if (qr >= a.Lq) break;
+    float mm = NEG_INF;
+    for (int s = 0; s < a.split; ++s) mm = fmaxf(mm, a.MLpart[((int64_t)(j0 + s) * 256 + row) * 2]);
+    float l = 0.f;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < a.split; ++s) {
+      const int64_t r = (int64_t)(j0 + s) * 256 + row;
+      const f32x2 ml = *(const f32x2*)(a.MLpart + r * 2);
+      const float wgt = ml[0] == NEG_INF ? 0.f : __builtin_amdgcn_exp2f(ml[0] - mm);
+      l += ml[1] * wgt;
+      o += *(const f32x4*)(a.Opart + r * HD + c) * wgt;
+    }
+    const float inv = 1.f / l;
+    bf16x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[r] * inv);
+    *(bf16x4*)(a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo + c) = v;
+    if (c == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = mm + log2f(l);
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Split-KV tail of the long-KV forward.  One workgroup per CU (144 KiB of LDS), so the grid
+// runs in rounds of #CU; when the last round is at most half full and every unit has many key
+// tiles, each of its `rem` units is split over `split` = #CU / rem (<= 8) workgroups: the final
+// round then fills the chip (720p x 81f: 11 560 units = 45 x 256 + 40 -> the last 40 units run
+// as 240 workgroups).  Returns the workspace bytes (0 = no split).
+#ifndef ATTN_TAIL_SPLIT
+#define ATTN_TAIL_SPLIT 1
+#endif
+int64_t tail_split(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, int& nmain,
+                   int& split) {
+  const int64_t nwg = ((Lq + 255) / 256) * H * B;
+  nmain = (int)nwg;
+  split = 1;
+  if (!ATTN_TAIL_SPLIT || Lk < 4096) return 0;
+  static int ncu[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const int64_t n = ncu[dev], rem = nwg % n, nkv = (k_len + 95) / 96;
+  if (nwg <= n || rem == 0 || 2 * rem > n) return 0;
+  split = (int)std::min<int64_t>(8, n / rem);
+  if (split < 2 || nkv < 4 * split) { split = 1; return 0; }
+  nmain = (int)(nwg - rem);
+  return rem * split * 256 * (HD * 4 + 8);
+}
 }  // namespace
 
+extern "C" int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                                          int64_t k_len) {
+  int nmain, split;
+  if (B <= 0 || Lq <= 0 || H <= 0 || Lk <= 0) return 0;
+  return tail_split(B, Lq, Lk, H, k_len, nmain, split);
+}
+
 // o = softmax(q k^T * scale, keys >= k_len masked) v ; lse2 = log2-domain row LSE.
-extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
-                             int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
-                             int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
-                             int64_t Lk, int64_t H, int64_t k_len, float scale, void* stream) {
+// ws: caller-owned scratch of prfl_attn_fwd_ws_bytes(...) bytes for the split-KV tail, or null
+// (no split).
+extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                                int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
+                                int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
+                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
+                                int64_t ws_bytes, void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
-  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || (ldq | ldk | ldv | ldo) % 8)
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(ws) ||
+      (ldq | ldk | ldv | ldo) % 8)
     return (int)hipErrorInvalidValue;
   if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535 ||
       ((Lq + 255) / 256) * H * B > 0x7fffffff || ((Lk + 255) / 256) * H * B > 0x7fffffff)
     return (int)hipErrorInvalidValue;
+  int nmain, split;
+  const int64_t need = tail_split(B, Lq, Lk, H, k_len, nmain, split);
+  if (!ws || ws_bytes < need) {                     // no (or too small a) workspace: no split
+    nmain = (int)(((Lq + 255) / 256) * H * B);
+    split = 1;
+  }
+  const int64_t nwg = ((Lq + 255) / 256) * H * B, rem = nwg - nmain;
+  float* Opart = (float*)ws;
+  float* MLpart = split > 1 ? Opart + rem * split * 256 * HD : nullptr;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f, (int)B};
+             scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
-  const dim3 grid((unsigned)(((Lq + 255) / 256) * H * B));
+  const dim3 grid((unsigned)(nmain + rem * split));
   if (kid == KID_ATTN_FWD)
     hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3>), grid, dim3(512), 0, s, a);
+  if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem), dim3(256), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                             int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
+                             int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
+                             int64_t Lk, int64_t H, int64_t k_len, float scale, void* stream) {
+  return prfl_attn_fwd_ws(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H,
+                          k_len, scale, nullptr, 0, stream);
 }
 
 // dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace.

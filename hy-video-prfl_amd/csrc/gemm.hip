@@ -10,11 +10,11 @@
 //
 // Three bf16 kernels, chosen by shape and epilogue (launch()): every element is summed in the
 // same k order (32-deep MFMA k-steps in sequence), so their outputs are bit-identical (tested):
-//   * gemm4w_kernel (the 720p projections: plain bf16, fp32 / accumulate, dGELU): 256x256 tile,
+//   * gemm4w_kernel (the 720p projections, every epilogue): 256x256 tile,
 //     4 waves = one per SIMD, each wave 128x128 with its 256 fp32 accumulators in AGPRs,
 //     operands by buffer LDS-DMA into a 4-slot ring of 32-deep K-slices (details at the kernel);
-//   * gemm256s_kernel (the 720p projections with the GELU or gated-residual epilogue): 256x256
-//     tile, 8 waves, staggered 4-phase LDS-DMA schedule (details at the kernel);
+//   * gemm256s_kernel (operands past 4 GiB, the fp8 path, tile code 512): 256x256 tile,
+//     8 waves, staggered 4-phase LDS-DMA schedule (details at the kernel);
 //   * gemm_kernel (small / ragged shapes): 128x128x64 tile, 4 waves (2x2), each 64x64 = 4x4
 //     MFMA 16x16x32 tiles, register-staged double buffer, one barrier per K step.
 // K-contiguous tiles live in LDS as rows with an XOR-swizzled 16-B chunk order and feed
@@ -546,13 +546,19 @@ __device__ __forceinline__ bf16x8 read_frag4(const char* lds, int base, int lane
 // Epilogue of the four-wave kernel: lane owns rows mb + 16 i (i < 8) and columns nb + 16 j + r
 // (j < 8, r < 4).  With one wave per SIMD nothing hides a load's latency, so (1) the per-column
 // bias / gate values are loaded once per lane (not once per row block), and (2) the per-element
-// inputs (fp32 / bf16 residual, fp32 accumulator, dGELU pre-activation) of row block i+1 are
-// loaded before row block i is computed and stored.  The in-place residual (res == C) stays
-// correct: a row block is read before anything of it is written.  Same arithmetic, in the same
-// order, as epilogue_tile (outputs bit-identical to the 128 kernel).
-template <int EPI>
+// inputs (fp32 / bf16 residual, fp32 accumulator, dGELU pre-activation) run EPI4_AHEAD row blocks
+// ahead of their use, kept in registers as loaded (bf16 inputs are widened only at their use, so
+// the prefetch is not drained by a conversion).  The main loop's fragment registers are dead
+// here, which leaves room for (EPI4_AHEAD + 1) x 32 input VGPRs.  The in-place residual
+// (res == C) stays correct: a row block is read before anything of it is written.  Same
+// arithmetic, in the same order, as epilogue_tile (outputs bit-identical to the 128 kernel).
+#ifndef EPI4_AHEAD
+#define EPI4_AHEAD 3
+#endif
+template <int EPI, bool IN_BF16>
 __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)[8][8], int mb, int nb) {
   constexpr bool HAS_IN = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_DGELU;
+  using InT = typename std::conditional<IN_BF16, bf16x4, f32x4>::type;
   float bias[8][4], gate[8][4];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -563,35 +569,33 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
       gate[j][r] = (EPI == EPI_RESID && g.gate && n < g.N) ? g.gate[n + r] : 1.f;
     }
   }
-  auto load_in = [&](int i, f32x4 (&in)[8]) {
+  const void* src = EPI == EPI_F32 ? (const void*)g.C : EPI == EPI_DGELU ? (const void*)g.aux : g.res;
+  const int64_t lds_in = EPI == EPI_F32 ? g.ldc : EPI == EPI_DGELU ? g.ldaux : g.ldr;
+  const bool any_in = HAS_IN && (EPI != EPI_F32 || g.accumulate);
+  auto load_in = [&](int i, InT (&in)[8]) {
     const int m = mb + 16 * i;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int n = nb + 16 * j;
-      in[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (m >= g.M || n >= g.N) continue;
-      if (EPI == EPI_F32) {
-        if (g.accumulate) in[j] = *(const f32x4*)((const float*)g.C + (int64_t)m * g.ldc + n);
-      } else if (EPI == EPI_DGELU) {
-        const bf16x4 pre = *(const bf16x4*)(g.aux + (int64_t)m * g.ldaux + n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) in[j][r] = bf2f(pre[r]);
-      } else if (EPI == EPI_RESID) {
-        if (g.res_bf16) {
-          const bf16x4 rr = *(const bf16x4*)((const bf16*)g.res + (int64_t)m * g.ldr + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) in[j][r] = bf2f(rr[r]);
-        } else {
-          in[j] = *(const f32x4*)((const float*)g.res + (int64_t)m * g.ldr + n);
-        }
-      }
+      in[j] = InT{};
+      if (!any_in || m >= g.M || n >= g.N) continue;
+      in[j] = *(const InT*)((const char*)src + ((int64_t)m * lds_in + n) * sizeof(in[j][0]));
     }
   };
-  f32x4 cur[8], nxt[8];
-  if (HAS_IN) load_in(0, cur);
+  auto widen = [](InT x) {
+    f32x4 f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = (float)x[r];
+    return f;
+  };
+  InT buf[8][8];
+  if (HAS_IN) {
+#pragma unroll
+    for (int i = 0; i < EPI4_AHEAD; ++i) load_in(i, buf[i]);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    if (HAS_IN && i + 1 < 8) load_in(i + 1, nxt);
+    if (HAS_IN && i + EPI4_AHEAD < 8) load_in(i + EPI4_AHEAD, buf[i + EPI4_AHEAD]);
     const int m = mb + 16 * i;
     if (m < g.M) {
 #pragma unroll
@@ -600,11 +604,12 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
         if (n >= g.N) continue;
         const f32x4 v = acc[i][j];
         if (EPI == EPI_F32) {
-          *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + cur[j] : v;
+          *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + widen(buf[i][j]) : v;
         } else if (EPI == EPI_DGELU) {
+          const f32x4 pre = widen(buf[i][j]);
           bf16x4 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(cur[j][r]));
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
           *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
         } else {
           float y[4];
@@ -631,17 +636,14 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
               for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
               *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
             }
+            const f32x4 res = widen(buf[i][j]);
             f32x4 o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = cur[j][r] + mul_rn(y[r], gate[j][r]);
+            for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gate[j][r]);
             *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
           }
         }
       }
-    }
-    if (HAS_IN) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
     }
   }
 }
@@ -738,28 +740,44 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // the MFMAs are inline asm: the compiler does not see their AGPR writes, so pad the
   // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  epilogue4w<EPI>(g, acc, m0 + wm * 128 + (lane & 15), n0 + wn * 128 + 4 * (lane >> 4));
+  const int mb = m0 + wm * 128 + (lane & 15), nb = n0 + wn * 128 + 4 * (lane >> 4);
+  if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
+    epilogue4w<EPI, true>(g, acc, mb, nb);
+  else
+    epilogue4w<EPI, false>(g, acc, mb, nb);
 }
 
-// tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced
+// tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced,
+// 512 = the 256 tile on the 8-wave kernel
 // (parity tests: both kernels accumulate every element in the same k order, so their outputs
 // are bit-identical)
+// GELU / gated-residual epilogues on the four-wave kernel (1) or the 8-wave one (0): with the
+// sigmoid-form GELU and the 3-row-block-ahead epilogue inputs the four-wave kernel is level on
+// FFN-up GELU (8.91 vs 8.92 ms) and 1-4 % faster on the residual (o-proj 3.66 vs 3.80 ms) at 720p
+// (profiles/r02_gemm_epi4w_ab.txt); round 2's first four-wave epilogue was 1-6 % slower there.
+#ifndef GEMM_GELU_4W
+#define GEMM_GELU_4W 1
+#endif
+#ifndef GEMM_RESID_4W
+#define GEMM_RESID_4W 1
+#endif
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
   // the 256 tiles need whole 64-deep K steps and whole 256-wide MN-major extents
   const bool fits256 = (g.K % BK) == 0 && g.K >= 128 && (A_KC || g.M % BM2 == 0) &&
                        (B_KC || g.N % BN2 == 0);
-  if (tile == 256 && !fits256) return (int)hipErrorInvalidValue;
-  if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
-    // GELU / gated-residual epilogues: the 8-wave kernel (its two waves per SIMD overlap the
-    // VALU-heavy tanh and the residual round trip; the four-wave kernel is 6 % / 1-3 % slower
-    // there, profiles/r02_gemm_4w_epilogues.txt).  Everything else: the four-wave kernel, which
-    // addresses each operand through a 32-bit buffer offset.
+  if ((tile == 256 || tile == 512) && !fits256) return (int)hipErrorInvalidValue;
+  if (tile == 512) {       // forced: the 8-wave 256 kernel (parity tests)
+    hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);
+  } else if (tile == 256 || (tile == 0 && fits256 && nt256 >= 96)) {
+    // the four-wave kernel (each operand addressed through a 32-bit buffer offset) wherever
+    // the operands fit 4 GiB; the 8-wave kernel otherwise (and for the epilogues switched back
+    // by GEMM_GELU_4W / GEMM_RESID_4W = 0)
     const int64_t bytes_a = (A_KC ? (int64_t)g.M : (int64_t)g.K) * g.lda * 2;
     const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
-    const bool four = EPI != EPI_GELU && EPI != EPI_RESID && bytes_a < (1ll << 32) &&
-                      bytes_b < (1ll << 32);
+    const bool four = (GEMM_GELU_4W || EPI != EPI_GELU) && (GEMM_RESID_4W || EPI != EPI_RESID) &&
+                      bytes_a < (1ll << 32) && bytes_b < (1ll << 32);
     if (four)
       hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
     else
@@ -781,7 +799,7 @@ extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, co
                                     void* aux, int64_t ldaux, int accumulate, int tile,
                                     void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (tile != 0 && tile != 128 && tile != 256) return (int)hipErrorInvalidValue;
+  if (tile != 0 && tile != 128 && tile != 256 && tile != 512) return (int)hipErrorInvalidValue;
   // K is a contiguous extent only for K-major operands; MN-major operands take any K (row tail)
   if (K <= 0 || ((a_kmajor || b_kmajor) && (K % 8) != 0) || (N % 4) != 0)
     return (int)hipErrorInvalidValue;

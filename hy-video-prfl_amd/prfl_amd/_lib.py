@@ -23,6 +23,9 @@ SIGNATURES = {
                              I32, P, I64, I32, I32, P],
     "prfl_attn_fwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
                       I64, F32, P],
+    "prfl_attn_fwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
+                         I64, F32, P, I64, P],
+    "prfl_attn_fwd_ws_bytes": [I64, I64, I64, I64, I64],
     "prfl_attn_bwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64,
                       I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],
@@ -52,6 +55,9 @@ SIGNATURES = {
     "prfl_prof_collect": [P, P, P, I32],
 }
 
+# entries that return a value other than a hipError_t code
+RESTYPES = {"prfl_attn_fwd_ws_bytes": I64}
+
 # kernel ids of the profiling hooks (csrc/common.h)
 KID = dict(gemm=0, attn_fwd=1, attn_fwd_short=2, attn_bwd_dkdv=3, attn_bwd_dq=4, ln=5, rms=6,
            eltwise=7, adamw=8, pool=9)
@@ -70,7 +76,7 @@ def load():
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = args
-            fn.restype = I32
+            fn.restype = RESTYPES.get(name, I32)
         _lib = lib
     return _lib
 

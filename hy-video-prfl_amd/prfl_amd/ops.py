@@ -22,7 +22,7 @@ def _ld(t):
 def gemm(a, b, c, M, N, K, a_kmajor=True, b_kmajor=True, epilogue=EPI_BF16, bias=None,
          gate=None, res=None, aux=None, accumulate=False, tile=0):
     """C[m][n] = sum_k A(m,k) B(n,k) (+ epilogue); see include/prfl_hip.h.  tile: 0 = by shape,
-    128 / 256 = forced (prfl_gemm_bf16_tiled)."""
+    128 / 256 (four-wave) / 512 (8-wave 256 tile) = forced (prfl_gemm_bf16_tiled)."""
     _lib.require_gpu(a, b, c)
     assert a.dtype == BF16 and b.dtype == BF16
     assert bias is None or (bias.dtype == BF16 and bias.is_contiguous())
@@ -218,9 +218,12 @@ def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None):
     if out is None:
         out = torch.empty(Lq, C, dtype=BF16, device=q.device)
     lse = torch.empty(num_heads, Lq, dtype=torch.float32, device=q.device)
-    call("prfl_attn_fwd", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
+    # scratch for the split-KV tail of long-KV launches (0 bytes when the grid has no tail)
+    nb = _lib.load().prfl_attn_fwd_ws_bytes(1, Lq, Lk, num_heads, k_len)
+    ws = torch.empty(nb, dtype=torch.uint8, device=q.device) if nb > 0 else None
+    call("prfl_attn_fwd_ws", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
          I64(_ld(v)), I64(0), ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk),
-         I64(num_heads), I64(k_len), F32(sc), stream_ptr())
+         I64(num_heads), I64(k_len), F32(sc), ptr(ws), I64(nb), stream_ptr())
     return out, lse
 
 

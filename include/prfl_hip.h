@@ -44,9 +44,10 @@ int prfl_gemm_bf16(const void* A, int64_t lda, int a_kmajor, const void* B, int6
                    int64_t ldr, int res_bf16, void* aux, int64_t ldaux, int accumulate,
                    void* stream);
 /* The same GEMM with the tile chosen by the caller: tile = 0 (by shape, as prfl_gemm_bf16),
- * 128 (128x128 tile, 4 waves) or 256 (256x256 tile, 8 waves, staggered LDS-DMA ring; needs
- * K % 64 == 0 and MN-major extents % 256 == 0, else hipErrorInvalidValue).  Both kernels sum
- * every output element in the same k order, so their results are bit-identical. */
+ * 128 (128x128 tile, 4 waves), 256 (256x256 tile, four-wave kernel with AGPR accumulators) or
+ * 512 (256x256 tile, 8-wave staggered-ring kernel); 256 / 512 need K % 64 == 0 and MN-major
+ * extents % 256 == 0, else hipErrorInvalidValue.  All kernels sum every output element in the
+ * same k order, so their results are bit-identical. */
 int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
                          int b_kmajor, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
                          int epilogue, const void* bias, const float* gate, const void* res,
@@ -63,6 +64,16 @@ int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                   const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
                   float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
                   float scale, void* stream);
+/* The same with a caller-owned scratch buffer `ws` of prfl_attn_fwd_ws_bytes(B, Lq, Lk, H, k_len)
+ * bytes (16-B aligned; null or smaller = prfl_attn_fwd): long-KV launches whose last dispatch
+ * round would run only a few workgroups split those units' key tiles over several workgroups
+ * and merge the partial softmax states (flash-decoding), so the final round fills the chip. */
+int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                     int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
+                     int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                     int64_t k_len, float scale, void* ws, int64_t ws_bytes, void* stream);
+/* Scratch bytes prfl_attn_fwd_ws needs on the current device (0 = no split for this shape). */
+int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
 /* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
  * caller-owned workspace. */
 int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "prfl_hip.h")).read()
-    return sorted(set(re.findall(r"\bint\s+(prfl_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|int64_t)\s+(prfl_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_abi_library_exports_header():

@@ -20,6 +20,11 @@ def load(path):
     lib = ctypes.CDLL(os.path.abspath(path))
     lib.prfl_attn_fwd.argtypes, lib.prfl_attn_fwd.restype = FWD, ctypes.c_int
     lib.prfl_attn_bwd.argtypes, lib.prfl_attn_bwd.restype = BWD, ctypes.c_int
+    lib.has_ws = hasattr(lib, "prfl_attn_fwd_ws")
+    if lib.has_ws:   # split-KV tail builds: forward with a caller-owned workspace
+        lib.prfl_attn_fwd_ws.argtypes, lib.prfl_attn_fwd_ws.restype = FWD[:-1] + [P, I64, P], ctypes.c_int
+        lib.prfl_attn_fwd_ws_bytes.argtypes = [I64] * 5
+        lib.prfl_attn_fwd_ws_bytes.restype = I64
     return lib
 
 

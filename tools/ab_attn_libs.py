@@ -32,8 +32,15 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
 
     def fwd(lib, b):
-        assert lib.prfl_attn_fwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
-                                 b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc, st) == 0
+        args = (q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc)
+        if lib.has_ws:
+            nb = lib.prfl_attn_fwd_ws_bytes(1, L, L, H, L)
+            if "ws" not in b or b["ws"].numel() < nb:
+                b["ws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+            assert lib.prfl_attn_fwd_ws(*args, b["ws"].data_ptr(), nb, st) == 0
+        else:
+            assert lib.prfl_attn_fwd(*args, st) == 0
 
     def bwd(lib, b):
         assert lib.prfl_attn_bwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,

@@ -15,7 +15,7 @@ for f in sorted(glob.glob(os.path.join(root, "*", "pmc_counter_collection.csv"))
         if "at::" in name:
             continue
         if "anonymous namespace)::" in name:
-            short = name.split("::")[1].split("(")[0]
+            short = name.split("::")[1].split("((")[0].split("(")[0] if "<" not in name else name.split("::")[1].split(">(")[0] + ">"
         else:                      # a library kernel (hipBLASLt Cijk_...): keep its name head
             short = name[:72]
         acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))

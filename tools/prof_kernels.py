@@ -82,6 +82,28 @@ elif which == "gemm720":
             dt = time.time() - t0
             print(f"gemm dw  {name} {N}x{K}x{M} {dt*1e3:.2f} ms  {2*M*N*K/dt/1e12:.0f} TF/s", flush=True)
         del x, w, y, dy
+elif which == "gemmepi":
+    # the fused-epilogue forward GEMMs of a 720p block (o-proj gated residual, FFN-up GELU with
+    # the pre-activation store, FFN-down gated residual), one dispatch each per rep, for PMC runs
+    for name, N, K, epi in (("o_resid", C, C, ops.EPI_RESID), ("ffn1_gelu", F, C, ops.EPI_GELU),
+                            ("ffn2_resid", C, F, ops.EPI_RESID)):
+        x = torch.randn(L, K, device=dev, generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        aux = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+        if epi == ops.EPI_RESID:
+            res = torch.randn(L, N, device=dev, generator=g)
+            gate = torch.randn(N, device=dev, generator=g)
+            kw = dict(gate=gate, res=res, aux=aux)
+        else:
+            kw = dict(aux=aux)
+        for i in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            ops.linear(x, w, None, epi, **kw)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"gemm {name} {L}x{N}x{K} {dt*1e3:.2f} ms  {2*L*N*K/dt/1e12:.0f} TF/s", flush=True)
+        del x, w, aux, kw
 elif which == "gemmcmp":
     # the QKV forward GEMM through prfl_gemm and through torch.matmul (hipBLASLt), same operands:
     # PMC comparison of MFMA busy, clock (GRBM_GUI_ACTIVE / 8 / wall) and instruction mix
