@@ -585,24 +585,25 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // K / V tile by LDS-DMA: NKT * 8 + NKT * 8 pieces of 4 rows, NKT + NKT per wave, swizzles on
   // the source; buffer resources rebased per tile keep the per-lane offsets 32-bit and loop
   // invariant, rows past Lk land as zeros (masked: they are past k_len)
-  uint32_t vok[NKT], vov[NKT];
-#pragma unroll
-  for (int i = 0; i < NKT; ++i) {
-    const int row = (w * NKT + i) * 4 + (lane >> 4), pc = lane & 15;
-    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-    vok[i] = (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4);
-    vov[i] = (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4);
-  }
+  // (the per-lane offsets are re-derived at every tile from a volatile lane id: kept live across
+  // the loop they pushed this kernel one VGPR past 256, and the spill's reload + vmcnt(0) sat in
+  // front of every tile's DMA issue)
   auto dma = [&](int t, int st) {
     char* Ks = smem + st * SB;
     char* Vs = Ks + SV;
     const int rows = min(a.Lk - t * TK, TK);
     const i32x4 sk = make_srd(Kb + (int64_t)t * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
     const i32x4 sv = make_srd(Vb + (int64_t)t * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
+    uint32_t ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
     for (int i = 0; i < NKT; ++i) {
-      dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
-      dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
+      const int row = (w * NKT + i) * 4 + (ln >> 4), pc = ln & 15;
+      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
+      dma16_buf(sk, (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4), 0,
+                lds_addr(Ks + (w * NKT + i) * 1024));
+      dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4), 0,
+                lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
   dma(0, 0);
