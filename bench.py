@@ -132,10 +132,10 @@ def cpu_baseline(L_sample=4096):
 
 def pmc_traffic(L):
     """HBM-side bytes per launch of the roofline kernel from the committed rocprofv3 --pmc passes
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/r02_pmc_attn_fwd720_xcd.txt, measured on
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/r02_pmc_attn_fwd720_split.txt, measured on
     the isolated 720p self-attention forward, the kernel the bench runs).  PMC counters cannot be
     read inside this process."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_attn_fwd720_xcd.txt")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_attn_fwd720_split.txt")
     if L != 73920 or not os.path.exists(path):
         return None, None
     for line in open(path):

@@ -296,12 +296,15 @@ constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
 constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
 
 
+#ifndef GEMM_GROUP_M
+#define GEMM_GROUP_M 4        // 256-row blocks walked together per XCD (L2 / MALL reuse of B)
+#endif
 __device__ __forceinline__ void tile_coords2(int bid, int M, int N, int& tm, int& tn) {
   const int ntm = (M + BM2 - 1) / BM2, ntn = (N + BN2 - 1) / BN2;
   const int nwg = ntm * ntn;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int GM = 4;
+  const int GM = GEMM_GROUP_M;
   const int group = w / (GM * ntn);
   const int first_m = group * GM;
   const int gsz = min(ntm - first_m, GM);
