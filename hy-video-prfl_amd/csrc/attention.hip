@@ -674,8 +674,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
 }
 
-// Merge of the split-KV tail partials: one workgroup per split unit, 8 query rows per pass (32
-// lanes x 4 columns per row): m = max_s m_s, l = sum_s l_s 2^(m_s - m), O = sum_s O_s 2^(m_s - m)
+// Merge of the split-KV tail partials: 8 workgroups per split unit, 32 query rows each, 8 rows
+// per pass (32 lanes x 4 columns per row): m = max_s m_s, l = sum_s l_s 2^(m_s - m), O = sum_s O_s 2^(m_s - m)
 // / l, lse2 = m + log2(l) -- the flash-decoding combination of the per-share online softmax.
 __global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
   const int unit = a.nmain + blockIdx.x;
@@ -684,7 +684,8 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
   const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
   const int c = (threadIdx.x & 31) * 4;
   const int j0 = blockIdx.x * a.split;
-  for (int row = threadIdx.x >> 5; row < 256; row += 8) {
+  const int r0 = blockIdx.y * 32;          // 8 workgroups per unit, 32 rows each
+  for (int row = r0 + (threadIdx.x >> 5); row < r0 + 32; row += 8) {
     const int qr = q0 + row;
     if (qr >= a.Lq) break;
     float mm = NEG_INF;
@@ -780,7 +781,7 @@ extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const vo
     hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3>), grid, dim3(512), 0, s, a);
-  if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem), dim3(256), 0, s, a);
+  if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();
