@@ -55,7 +55,22 @@ struct AttnBwdArgs {
   int Lq, Lk, H, k_len;
   float sl2, scale;
   int B;
+  // split tails (see prfl_attn_bwd_ws): dK/dV workgroups >= nmain_k each take 1/split_k of the
+  // query tiles of one of the last key-tile units, dQ workgroups >= nmain_q 1/split_q of the key
+  // tiles of one of the last query-tile units; unscaled fp32 partials, summed by the merges
+  int nmain_k, split_k, nmain_q, split_q;
+  float* Pk;             // [dK/dV tail wg][256 keys][128] fp32 (dK^T partial)
+  float* Pv;             // [dK/dV tail wg][256 keys][128] fp32
+  float* Pq;             // [dQ tail wg][256 queries][128] fp32
 };
+
+// (unit, share) of a 1-D grid whose workgroups >= nmain split the last units `split` ways
+__device__ __forceinline__ void tail_unit(int nmain, int split, int& unit, int& share, bool& part) {
+  const int bid = blockIdx.x;
+  part = bid >= nmain;
+  unit = part ? nmain + (bid - nmain) / split : bid;
+  share = part ? (bid - nmain) % split : 0;
+}
 
 // LDS images (256-B rows of 128 bf16):
 //  swz16: chunk ^ (row & 15)            -> conflict-free ds_read_b128 row reads
@@ -399,7 +414,11 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   constexpr int V_BYTES = 256 * 256, STAGE = 16384 * 2 + 512;
   __shared__ __attribute__((aligned(16))) char smem[V_BYTES + 2 * STAGE];
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 256;
+  int unit, share;
+  bool part;
+  tail_unit(a.nmain_k, a.split_k, unit, share, part);
+  const int nkt = (a.Lk + 255) / 256;
+  const int b = unit / (nkt * a.H), h = (unit / nkt) % a.H, k0 = (unit % nkt) * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
@@ -436,10 +455,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     voq[i] = (uint32_t)(row * a.ldq * 2) + ((pc ^ swzb) << 4);
     vod[i] = (uint32_t)(row * a.lddo * 2) + ((pc ^ swzb) << 4);
   }
-  auto dma_tile = [&](int t, int st) {
+  // query tiles [t0, t0 + nq) of this workgroup
+  int t0 = 0, nq = (a.Lq + 63) / 64;
+  if (part) {
+    const int per = (nq + a.split_k - 1) / a.split_k;
+    t0 = min(share * per, nq);
+    nq = min(nq, t0 + per) - t0;
+  }
+  auto dma_tile = [&](int t, int st) {     // local tile t = query tile t0 + t
     char* Qs = smem + V_BYTES + st * STAGE;
     char* Ds = Qs + 16384;
-    const int qb = t * 64, rows = min(a.Lq - qb, 64);   // the record range stays < 2^32 bytes
+    const int qb = (t0 + t) * 64, rows = min(a.Lq - qb, 64);   // record range < 2^32 bytes
     const i32x4 sq = make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2));
     const i32x4 sd = make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2));
 #pragma unroll
@@ -460,8 +486,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-  const int nq = (a.Lq + 63) / 64;
-  dma_tile(0, 0);
+  if (nq > 0) dma_tile(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): K fragments, V, tile 0
   __syncthreads();
   for (int t = 0; t < nq; ++t) {
@@ -470,7 +495,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     const char* Qs = smem + V_BYTES + st * STAGE;
     const char* Ds = Qs + 16384;
     const float* Ls = (const float*)(Qs + 32768);
-    const int qb = t * 64;
+    const int qb = (t0 + t) * 64;
     const bool tail = qb + 64 > a.Lq;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -531,7 +556,19 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  if (key < a.Lk) {
+  if (part) {            // unscaled partial dK^T / dV^T of this query share (attn_merge_kv)
+    const int64_t r = (int64_t)(blockIdx.x - a.nmain_k) * 256 + w * 32 + l32;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int c = dt * 32 + 8 * rg + 4 * hh;
+        *(f32x4*)(a.Pk + r * HD + c) =
+            (f32x4){dk[dt][rg * 4], dk[dt][rg * 4 + 1], dk[dt][rg * 4 + 2], dk[dt][rg * 4 + 3]};
+        *(f32x4*)(a.Pv + r * HD + c) =
+            (f32x4){dv[dt][rg * 4], dv[dt][rg * 4 + 1], dv[dt][rg * 4 + 2], dv[dt][rg * 4 + 3]};
+      }
+  } else if (key < a.Lk) {
     bf16* dKb = a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk;
     bf16* dVb = a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv;
 #pragma unroll
@@ -558,7 +595,11 @@ template <int NKT>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
   __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 256;
+  int unit, share;
+  bool part;
+  tail_unit(a.nmain_q, a.split_q, unit, share, part);
+  const int nqt = (a.Lq + 255) / 256;
+  const int b = unit / (nqt * a.H), h = (unit / nqt) % a.H, q0 = (unit % nqt) * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
@@ -581,16 +622,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-  const int nkv = (a.k_len + TK - 1) / TK;
+  // key tiles [t0, t0 + nkv) of this workgroup
+  int t0 = 0, nkv = (a.k_len + TK - 1) / TK;
+  if (part) {
+    const int per = (nkv + a.split_q - 1) / a.split_q;
+    t0 = min(share * per, nkv);
+    nkv = min(nkv, t0 + per) - t0;
+  }
   // K / V tile by LDS-DMA: NKT * 8 + NKT * 8 pieces of 4 rows, NKT + NKT per wave, swizzles on
   // the source; buffer resources rebased per tile keep the per-lane offsets 32-bit and loop
   // invariant, rows past Lk land as zeros (masked: they are past k_len)
   // (the per-lane offsets are re-derived at every tile from a volatile lane id: kept live across
   // the loop they pushed this kernel one VGPR past 256, and the spill's reload + vmcnt(0) sat in
   // front of every tile's DMA issue)
-  auto dma = [&](int t, int st) {
+  auto dma = [&](int tl, int st) {     // local tile tl = key tile t0 + tl
     char* Ks = smem + st * SB;
     char* Vs = Ks + SV;
+    const int t = t0 + tl;
     const int rows = min(a.Lk - t * TK, TK);
     const i32x4 sk = make_srd(Kb + (int64_t)t * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
     const i32x4 sv = make_srd(Vb + (int64_t)t * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
@@ -606,11 +654,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                 lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
-  dma(0, 0);
+  if (nkv > 0) dma(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
   __syncthreads();
   for (int t = 0; t < nkv; ++t) {
-    const int kb = t * TK;
+    const int kb = (t0 + t) * TK;
     // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
     if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
     const char* Ks = smem + (t & 1) * SB;
@@ -660,7 +708,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     asm volatile("" ::: "memory");
   }
   const int qo = q0 + w * 32 + l32;
-  if (qo < a.Lq) {
+  if (part) {            // unscaled partial dQ^T of this key share (attn_merge_q)
+    const int64_t r = (int64_t)(blockIdx.x - a.nmain_q) * 256 + w * 32 + l32;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+        *(f32x4*)(a.Pq + r * HD + dt * 32 + 8 * rg + 4 * hh) =
+            (f32x4){dq[dt][rg * 4], dq[dt][rg * 4 + 1], dq[dt][rg * 4 + 2], dq[dt][rg * 4 + 3]};
+  } else if (qo < a.Lq) {
     bf16* dQb = a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -708,6 +764,51 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
   }
 }
 
+// Sums of the backward's split-tail partials: 8 workgroups per unit, 32 rows each, 8 rows per
+// pass (32 lanes x 4 columns per row).  dK = scale * sum_s dK_s (keys >= k_len: 0), dV = sum_s
+// dV_s; dQ = scale * sum_s dQ_s.
+__global__ __launch_bounds__(256) void attn_merge_kv_kernel(AttnBwdArgs a) {
+  const int unit = a.nmain_k + blockIdx.x, nkt = (a.Lk + 255) / 256;
+  const int b = unit / (nkt * a.H), h = (unit / nkt) % a.H, k0 = (unit % nkt) * 256;
+  const int c = (threadIdx.x & 31) * 4, r0 = blockIdx.y * 32;
+  for (int row = r0 + (threadIdx.x >> 5); row < r0 + 32; row += 8) {
+    const int key = k0 + row;
+    if (key >= a.Lk) break;
+    f32x4 sk = {0.f, 0.f, 0.f, 0.f}, sv = {0.f, 0.f, 0.f, 0.f};
+    for (int sh = 0; sh < a.split_k; ++sh) {
+      const int64_t r = ((int64_t)blockIdx.x * a.split_k + sh) * 256 + row;
+      sk += *(const f32x4*)(a.Pk + r * HD + c);
+      sv += *(const f32x4*)(a.Pv + r * HD + c);
+    }
+    const bool kvalid = key < a.k_len;
+    bf16x4 vk, vv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vk[r] = f2bf(kvalid ? sk[r] * a.scale : 0.f);
+      vv[r] = f2bf(kvalid ? sv[r] : 0.f);
+    }
+    *(bf16x4*)(a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk + c) = vk;
+    *(bf16x4*)(a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv + c) = vv;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_merge_q_kernel(AttnBwdArgs a) {
+  const int unit = a.nmain_q + blockIdx.x, nqt = (a.Lq + 255) / 256;
+  const int b = unit / (nqt * a.H), h = (unit / nqt) % a.H, q0 = (unit % nqt) * 256;
+  const int c = (threadIdx.x & 31) * 4, r0 = blockIdx.y * 32;
+  for (int row = r0 + (threadIdx.x >> 5); row < r0 + 32; row += 8) {
+    const int qo = q0 + row;
+    if (qo >= a.Lq) break;
+    f32x4 sq = {0.f, 0.f, 0.f, 0.f};
+    for (int sh = 0; sh < a.split_q; ++sh)
+      sq += *(const f32x4*)(a.Pq + (((int64_t)blockIdx.x * a.split_q + sh) * 256 + row) * HD + c);
+    bf16x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = f2bf(sq[r] * a.scale);
+    *(bf16x4*)(a.dQ + b * a.bdq + h * HD + (int64_t)qo * a.lddq + c) = v;
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Split-KV tail of the long-KV forward.  One workgroup per CU (144 KiB of LDS), so the grid
@@ -718,23 +819,47 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 #ifndef ATTN_TAIL_SPLIT
 #define ATTN_TAIL_SPLIT 1
 #endif
-int64_t tail_split(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, int& nmain,
-                   int& split) {
-  const int64_t nwg = ((Lq + 255) / 256) * H * B;
-  nmain = (int)nwg;
+// nunits units of nwork tiles each, one workgroup per CU: when the last dispatch round is at
+// most half full, split its rem units `split` = #CU / rem (<= 8) ways (each share >= 4 tiles).
+// Returns rem (0 = no split); nmain = the workgroups that take a whole unit.
+int64_t tail_units(int64_t nunits, int64_t nwork, int& nmain, int& split) {
+  nmain = (int)nunits;
   split = 1;
-  if (!ATTN_TAIL_SPLIT || Lk < 4096) return 0;
+  if (!ATTN_TAIL_SPLIT) return 0;
   static int ncu[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
   if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  const int64_t n = ncu[dev], rem = nwg % n, nkv = (k_len + 95) / 96;
-  if (nwg <= n || rem == 0 || 2 * rem > n) return 0;
+  const int64_t n = ncu[dev], rem = nunits % n;
+  if (nunits <= n || rem == 0 || 2 * rem > n) return 0;
   split = (int)std::min<int64_t>(8, n / rem);
-  if (split < 2 || nkv < 4 * split) { split = 1; return 0; }
-  nmain = (int)(nwg - rem);
+  if (split < 2 || nwork < 4 * split) { split = 1; return 0; }
+  nmain = (int)(nunits - rem);
+  return rem;
+}
+
+// forward (long KV only): units = query tiles, work = 96-key tiles; workspace bytes
+int64_t tail_split(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, int& nmain,
+                   int& split) {
+  const int64_t units = ((Lq + 255) / 256) * H * B;
+  nmain = (int)units;
+  split = 1;
+  if (Lk < 4096) return 0;
+  const int64_t rem = tail_units(units, (k_len + 95) / 96, nmain, split);
   return rem * split * 256 * (HD * 4 + 8);
+}
+
+// backward (long KV only): dK/dV units = key tiles over 64-query tiles, dQ units = query tiles
+// over 96-key tiles; workspace = dK + dV partials, then dQ partials
+int64_t tail_split_bwd(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
+                       int& nmain_k, int& split_k, int& nmain_q, int& split_q) {
+  const int64_t uk = ((Lk + 255) / 256) * H * B, uq = ((Lq + 255) / 256) * H * B;
+  nmain_k = (int)uk; nmain_q = (int)uq; split_k = split_q = 1;
+  if (Lk < 4096) return 0;
+  const int64_t rk = tail_units(uk, (Lq + 63) / 64, nmain_k, split_k);
+  const int64_t rq = tail_units(uq, (k_len + 95) / 96, nmain_q, split_q);
+  return (2 * rk * split_k + rq * split_q) * 256 * HD * 4;
 }
 }  // namespace
 
@@ -796,23 +921,35 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
                           k_len, scale, nullptr, 0, stream);
 }
 
-// dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace.
-extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
-                             int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
-                             int64_t ldo, int64_t bo, const void* dout, int64_t lddo, int64_t bdo,
-                             const float* lse2, float* delta, void* dq, int64_t lddq, int64_t bdq,
-                             void* dk, int64_t lddk, int64_t bdk, void* dv, int64_t lddv,
-                             int64_t bdv, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
-                             int64_t k_len, float scale, void* stream) {
+// dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace; ws: caller-owned
+// scratch of prfl_attn_bwd_ws_bytes(...) bytes for the split tails, or null (no split).
+extern "C" int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                                int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
+                                int64_t ldo, int64_t bo, const void* dout, int64_t lddo,
+                                int64_t bdo, const float* lse2, float* delta, void* dq,
+                                int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
+                                void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
+                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
+                                int64_t ws_bytes, void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
-      !aligned16(dq) || !aligned16(dk) || !aligned16(dv) ||
+      !aligned16(dq) || !aligned16(dk) || !aligned16(dv) || !aligned16(ws) ||
       (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8)
     return (int)hipErrorInvalidValue;
   if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535 ||
       ((Lq + 255) / 256) * H * B > 0x7fffffff || ((Lk + 255) / 256) * H * B > 0x7fffffff)
     return (int)hipErrorInvalidValue;
+  int nmain_k, split_k, nmain_q, split_q;
+  const int64_t need = tail_split_bwd(B, Lq, Lk, H, k_len, nmain_k, split_k, nmain_q, split_q);
+  const int64_t uk = ((Lk + 255) / 256) * H * B, uq = ((Lq + 255) / 256) * H * B;
+  if (!ws || ws_bytes < need) {                     // no (or too small a) workspace: no split
+    nmain_k = (int)uk; nmain_q = (int)uq; split_k = split_q = 1;
+  }
+  const int64_t rk = uk - nmain_k, rq = uq - nmain_q;
+  float* Pk = (float*)ws;
+  float* Pv = Pk + rk * split_k * 256 * HD;
+  float* Pq = Pv + rk * split_k * 256 * HD;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nrows = B * Lq * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((nrows + 15) / 16), dim3(256), 0, s,
@@ -822,16 +959,38 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
   AttnBwdArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
-                scale * 1.4426950408889634f, scale, (int)B};
+                scale * 1.4426950408889634f, scale, (int)B, nmain_k, split_k, nmain_q, split_q,
+                Pk, Pv, Pq};
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((Lk + 255) / 256, H, B), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((unsigned)(nmain_k + rk * split_k)), dim3(512), 0, s, a);
+  if (rk) hipLaunchKernelGGL(attn_merge_kv_kernel, dim3((unsigned)rk, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();
   prfl_prof::begin(KID_ATTN_BWD_DQ, s);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3((Lq + 255) / 256, H, B), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
+  if (rq) hipLaunchKernelGGL(attn_merge_q_kernel, dim3((unsigned)rq, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                                          int64_t k_len) {
+  int nk, sk, nq, sq;
+  if (B <= 0 || Lq <= 0 || H <= 0 || Lk <= 0) return 0;
+  return tail_split_bwd(B, Lq, Lk, H, k_len, nk, sk, nq, sq);
+}
+
+extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                             int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
+                             int64_t ldo, int64_t bo, const void* dout, int64_t lddo, int64_t bdo,
+                             const float* lse2, float* delta, void* dq, int64_t lddq, int64_t bdq,
+                             void* dk, int64_t lddk, int64_t bdk, void* dv, int64_t lddv,
+                             int64_t bdv, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                             int64_t k_len, float scale, void* stream) {
+  return prfl_attn_bwd_ws(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, dout, lddo, bdo, lse2,
+                          delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
+                          scale, nullptr, 0, stream);
 }

@@ -26,6 +26,10 @@ SIGNATURES = {
     "prfl_attn_fwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
                          I64, F32, P, I64, P],
     "prfl_attn_fwd_ws_bytes": [I64, I64, I64, I64, I64],
+    "prfl_attn_bwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P,
+                         I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, I64,
+                         P],
+    "prfl_attn_bwd_ws_bytes": [I64, I64, I64, I64, I64],
     "prfl_attn_bwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64,
                       I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],
@@ -56,7 +60,7 @@ SIGNATURES = {
 }
 
 # entries that return a value other than a hipError_t code
-RESTYPES = {"prfl_attn_fwd_ws_bytes": I64}
+RESTYPES = {"prfl_attn_fwd_ws_bytes": I64, "prfl_attn_bwd_ws_bytes": I64}
 
 # kernel ids of the profiling hooks (csrc/common.h)
 KID = dict(gemm=0, attn_fwd=1, attn_fwd_short=2, attn_bwd_dkdv=3, attn_bwd_dq=4, ln=5, rms=6,

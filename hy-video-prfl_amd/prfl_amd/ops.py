@@ -237,11 +237,14 @@ def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=No
     dk = torch.empty(Lk, C, dtype=BF16, device=dev) if dk is None else dk
     dv = torch.empty(Lk, C, dtype=BF16, device=dev) if dv is None else dv
     delta = torch.empty(num_heads, Lq, dtype=torch.float32, device=dev)
-    call("prfl_attn_bwd", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
+    # scratch for the split tails of long-KV launches (0 bytes when the grids have no tail)
+    nb = _lib.load().prfl_attn_bwd_ws_bytes(1, Lq, Lk, num_heads, k_len)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb > 0 else None
+    call("prfl_attn_bwd_ws", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
          I64(_ld(v)), I64(0), ptr(o), I64(_ld(o)), I64(0), ptr(do), I64(_ld(do)), I64(0), ptr(lse),
          ptr(delta), ptr(dq), I64(_ld(dq)), I64(0), ptr(dk), I64(_ld(dk)), I64(0), ptr(dv),
          I64(_ld(dv)), I64(0), I64(1), I64(Lq), I64(Lk), I64(num_heads), I64(k_len), F32(sc),
-         stream_ptr())
+         ptr(ws), I64(nb), stream_ptr())
     return dq, dk, dv
 
 

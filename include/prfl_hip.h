@@ -83,6 +83,20 @@ int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                   void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq, int64_t Lk,
                   int64_t H, int64_t k_len, float scale, void* stream);
 
+/* The same with a caller-owned scratch buffer `ws` of prfl_attn_bwd_ws_bytes(B, Lq, Lk, H, k_len)
+ * bytes (16-B aligned; null or smaller = prfl_attn_bwd): long-KV launches split the units of
+ * their last, under-filled dispatch round (dK/dV over query tiles, dQ over key tiles) and sum
+ * the unscaled fp32 partials. */
+int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                     int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o, int64_t ldo,
+                     int64_t bo, const void* dout, int64_t lddo, int64_t bdo, const float* lse2,
+                     float* delta, void* dq, int64_t lddq, int64_t bdq, void* dk, int64_t lddk,
+                     int64_t bdk, void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
+                     int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
+                     int64_t ws_bytes, void* stream);
+/* Scratch bytes prfl_attn_bwd_ws needs on the current device (0 = no split for this shape). */
+int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
+
 /* ---- single-query attention pooling (reward head) ----------------------------------------
  * Replaces the core of the 1-query nn.MultiheadAttention of QueryAttention
  * (diffusers_lite/utils/network.py:80; num_queries 1, 8 heads, E = 5120): per sample n and head

@@ -301,9 +301,9 @@ def test_attention_full_size_vs_reference(ops, L, H):
 
 
 def test_attention_split_tail(ops):
-    """Split-KV tail of the long-KV forward (prfl_attn_fwd_ws): L = 8100 (ragged last query
-    tile), k_len = 8000 < Lk, 9 heads -> 288 units on 256 CUs, so the last 32 units (head 8) run
-    as 8 key shares each + merge.  Units outside the tail are bit-identical to the unsplit
+    """Split tails of the long-KV attention (prfl_attn_fwd_ws / prfl_attn_bwd_ws): L = 8100
+    (ragged last query tile), k_len = 8000 < Lk, 9 heads -> 288 units on 256 CUs, so the last 32
+    units (head 8) run as 8 shares each + merge, forward and backward.  Units outside the tail are bit-identical to the unsplit
     launch; the tail rows match it to rounding and match an fp64 computation over all keys."""
     from prfl_amd import _lib
     L, H, klen = 8100, 9, 8000
@@ -336,6 +336,28 @@ def test_attention_split_tail(ops):
     assert rel(o1[rows.to(DEV), tail], exact) < 5e-3
     lse_exact = torch.logsumexp(s, -1) / math.log(2.0)
     assert (lse[8, rows.to(DEV)].double().cpu() - lse_exact).abs().max().item() < 1e-3
+    # backward (prfl_attn_bwd_ws): dK/dV units are 256-key tiles (32 per head, head 8 = the
+    # tail, split over query tiles), dQ units 256-query tiles (head 8 split over key tiles);
+    # same forward output for both so only the backward's tail handling differs
+    if _lib.load().prfl_attn_bwd_ws_bytes(1, L, L, H, klen) == 0:
+        return
+    do = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
+    dq, dk, dv = ops.attn_bwd(q, k, v, o1, do, lse1, H, k_len=klen)     # split tails
+    dq1, dk1, dv1 = (torch.empty_like(q) for _ in range(3))
+    delta = torch.empty(H, L, device=DEV)
+    _lib.call("prfl_attn_bwd", *[_lib.ptr(t) if torch.is_tensor(t) else _lib.I64(t) for t in (
+        q, C, 0, k, C, 0, v, C, 0, o1, C, 0, do, C, 0, lse1, delta, dq1, C, 0, dk1, C, 0, dv1, C,
+        0, 1, L, L, H, klen)], _lib.F32(128 ** -0.5), _lib.stream_ptr())       # unsplit
+    for x, x1 in ((dq, dq1), (dk, dk1), (dv, dv1)):
+        assert torch.equal(x[:, :8 * 128], x1[:, :8 * 128])
+        assert not torch.equal(x[:, tail], x1[:, tail])
+        assert rel(x[:, tail], x1[:, tail]) < 2e-3        # fp32 partial sums, one bf16 rounding
+    assert torch.equal(dk[klen:], torch.zeros_like(dk[klen:]))
+    assert torch.equal(dv[klen:], torch.zeros_like(dv[klen:]))
+    _, _, rdq, rdk, rdv = _attention_ref_gpu(q[:, tail], k[:klen, tail], v[:klen, tail],
+                                             do[:, tail], 1, 128 ** -0.5)
+    assert rel(dq[:, tail], rdq) < 2e-2
+    assert rel(dk[:klen, tail], rdk) < 2e-2 and rel(dv[:klen, tail], rdv) < 2e-2
 
 
 def test_attention_rescale_spike(ops):

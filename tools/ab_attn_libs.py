@@ -43,10 +43,17 @@ def main():
             assert lib.prfl_attn_fwd(*args, st) == 0
 
     def bwd(lib, b):
-        assert lib.prfl_attn_bwd(q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
-                                 b["o"].data_ptr(), C, 0, do.data_ptr(), C, 0, b["lse"].data_ptr(),
-                                 b["delta"].data_ptr(), b["dq"].data_ptr(), C, 0, b["dk"].data_ptr(), C, 0,
-                                 b["dv"].data_ptr(), C, 0, 1, L, L, H, L, sc, st) == 0
+        args = (q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+                b["o"].data_ptr(), C, 0, do.data_ptr(), C, 0, b["lse"].data_ptr(),
+                b["delta"].data_ptr(), b["dq"].data_ptr(), C, 0, b["dk"].data_ptr(), C, 0,
+                b["dv"].data_ptr(), C, 0, 1, L, L, H, L, sc)
+        if lib.has_bws:
+            nb = lib.prfl_attn_bwd_ws_bytes(1, L, L, H, L)
+            if "bws" not in b or b["bws"].numel() < nb:
+                b["bws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+            assert lib.prfl_attn_bwd_ws(*args, b["bws"].data_ptr(), nb, st) == 0
+        else:
+            assert lib.prfl_attn_bwd(*args, st) == 0
 
     work = [("fwd", fwd, 4 * L * L * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
     for w, fn, fl in work:
