@@ -40,6 +40,7 @@ struct AttnArgs {
   int nmain, split;
   float* Opart;          // [tail wg][256 q][128 d] unnormalised O (fp32)
   float* MLpart;         // [tail wg][256 q][2] (row max, row sum), log2 domain
+  unsigned long long* clk;   // prof clock slot (workgroup 0 writes cycles, ticks) or null
 };
 
 struct AttnBwdArgs {
@@ -169,6 +170,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   const int bid = blockIdx.x;
   const bool part = bid >= a.nmain;
   const int unit = part ? a.nmain + (bid - a.nmain) / a.split : bid;
+  const bool clk = a.clk != nullptr && bid == 0 && threadIdx.x == 0;
+  unsigned long long c0 = 0, w0 = 0;
+  if (clk) {
+    c0 = clock64();
+    w0 = wall_clock64();
+  }
   int bh, tile;
   xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile, unit);
   const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
@@ -350,6 +357,11 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     st = st == 2 ? 0 : st + 1;
   }
   if (gp == 0) bar();
+  if (clk) {               // effective shader clock over this workgroup's lifetime (prof.hip)
+    const unsigned long long c1 = clock64(), w1 = wall_clock64();
+    a.clk[0] = c1 - c0;
+    a.clk[1] = w1 - w0;
+  }
   lsum += __shfl_xor(lsum, 32, 64);
   const int qr = q0 + w * 32 + l32;
   if (part) {            // unnormalised partial (O, m, l) of this key share, merged by attn_merge
@@ -897,10 +909,11 @@ extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const vo
   float* MLpart = split > 1 ? Opart + rem * split * 256 * HD : nullptr;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart};
+             scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart, nullptr};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
+  if (kid == KID_ATTN_FWD) a.clk = prfl_prof::clk_slot();
   const dim3 grid((unsigned)(nmain + rem * split));
   if (kid == KID_ATTN_FWD)
     hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3>), grid, dim3(512), 0, s, a);

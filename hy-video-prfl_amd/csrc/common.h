@@ -185,6 +185,7 @@ namespace prfl_prof {
 void begin(int kid, hipStream_t s);
 void end(int kid, hipStream_t s);
 void set_work(double w);  // algorithmic FLOPs/bytes of the launch being timed
+unsigned long long* clk_slot();  // (cycles, 100 MHz ticks) slot for the next launch, or null
 }
 enum {
   KID_GEMM = 0, KID_ATTN_FWD, KID_ATTN_FWD_SHORT, KID_ATTN_BWD_DKDV, KID_ATTN_BWD_DQ, KID_LN, KID_RMS,

@@ -11,8 +11,6 @@
 // The column reductions of the backward passes (d scale, d shift, d w, d b) are written as
 // per-workgroup partial rows and summed by colsum_reduce (elementwise.hip) — no float atomics,
 // bitwise reproducible.
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace {
@@ -29,73 +27,7 @@ __device__ __forceinline__ f32x4 ld4(const void* p, int64_t i, int is_bf16) {
 __device__ __forceinline__ f32x4 ldf4(const float* p, int i) { return *(const f32x4*)(p + i); }
 
 // --------------------------------------------------------------------------- LN + modulate --
-// One wave per row (4 rows per 256-thread workgroup): the row (C <= 5120 -> 20 float4 chunks per
-// lane) stays in registers, both reductions are wave shuffles (no LDS, no barriers), so a CU keeps
-// many rows in flight and the kernel streams at HBM rate.  Two-pass mean / variance as before.
 constexpr int WV = 20;  // float4 chunks per lane -> C <= 5120
-__global__ __launch_bounds__(NT) void ln_mod_fwd_kernel(
-    const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
-    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ w,
-    const float* __restrict__ b, float eps, bf16* __restrict__ out, int64_t ldo,
-    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-  if (row >= L) return;
-  const int lane = threadIdx.x & 63;
-  const int nc = C / 4;
-  f32x4 v[WV];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < WV; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
-      v[j] = ld4(x, row * ldx + c * 4, x_bf16);
-      s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
-    }
-  }
-  const float mean = wave_sum(s) / C;
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < WV; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float d = v[j][r] - mean;
-        ss += d * d;
-      }
-    }
-  }
-  const float var = wave_sum(ss) / C;
-  const float rstd = rsqrtf(var + eps);
-#pragma unroll
-  for (int j = 0; j < WV; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
-      bf16x4 o;
-      f32x4 a = w ? ldf4(w, c * 4) : (f32x4){0, 0, 0, 0};
-      f32x4 bb = b ? ldf4(b, c * 4) : (f32x4){0, 0, 0, 0};
-      f32x4 sc = scale ? ldf4(scale, c * 4) : (f32x4){0, 0, 0, 0};
-      f32x4 sh = shift ? ldf4(shift, c * 4) : (f32x4){0, 0, 0, 0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float xh = (v[j][r] - mean) * rstd;
-        float y;
-        if (w) {
-          y = mul_rn(xh, a[r]) + bb[r];
-        } else {
-          if (x_bf16) xh = bfr(xh);  // WanLayerNorm.type_as(x) for a bf16 input
-          y = mul_rn(xh, 1.f + sc[r]) + sh[r];
-        }
-        o[r] = f2bf(y);
-      }
-      *(bf16x4*)(out + row * ldo + c * 4) = o;
-    }
-  }
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
-  }
-}
 
 // dx (+)= LN backward; partial column sums: part0 = sum dy*xhat_used (d scale / d w),
 // part1 = sum dy (d shift / d b).  ROWS rows per workgroup.
@@ -311,9 +243,10 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
   }
 }
 
-// Same arithmetic as ln_mod_fwd_kernel with the per-column coefficients — (1 + scale, shift) or
-// (w, b) — staged once per workgroup in LDS and each wave normalising RPW rows in turn: the
-// one-row-per-wave kernel re-read 8 B of coefficients from L2 for every 4 B of x.
+// LN + modulate forward: one wave per row, the row (C <= 5120 -> 20 float4 chunks per lane) held
+// in registers, both reductions wave shuffles (two-pass mean / variance); the per-column
+// coefficients — (1 + scale, shift) or (w, b) — are staged once per workgroup in LDS and each wave
+// normalises RPW rows in turn (re-reading them from L2 per row cost 8 B for every 4 B of x).
 constexpr int RPW = 4;   // rows per wave -> 16 rows per workgroup
 __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
     const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
@@ -399,15 +332,9 @@ extern "C" int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L
   if (bad_c(C) || (!w && (!scale || !shift))) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  static const bool one_row = getenv("PRFL_LN_ONEROW") != nullptr;
-  if (one_row)
-    hipLaunchKernelGGL(ln_mod_fwd_kernel, dim3((L + NT / 64 - 1) / (NT / 64)), dim3(NT), 0, s, x,
-                       x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps, (bf16*)out, ldo, mean,
-                       rstd);
-  else
-    hipLaunchKernelGGL(ln_mod_fwd_lds_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
-                       dim3(NT), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps,
-                       (bf16*)out, ldo, mean, rstd);
+  hipLaunchKernelGGL(ln_mod_fwd_lds_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
+                     dim3(NT), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps,
+                     (bf16*)out, ldo, mean, rstd);
   prfl_prof::set_work((double)L * C * ((x_bf16 ? 2 : 4) + 2));
   prfl_prof::end(KID_LN, s);
   PRFL_LAUNCH_CHECK();

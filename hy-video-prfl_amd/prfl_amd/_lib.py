@@ -57,6 +57,7 @@ SIGNATURES = {
                             I64, P, I64, P],
     "prfl_prof_enable": [I32],
     "prfl_prof_collect": [P, P, P, I32],
+    "prfl_prof_clock": [P, P, P, P],
 }
 
 # entries that return a value other than a hipError_t code

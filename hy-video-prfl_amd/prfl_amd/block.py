@@ -39,10 +39,12 @@ def param_names(i2v):
 # a block whose forward records a graph may keep its self-attention output and LSE (L*C*2 +
 # H*L*4 bytes per sample) so the backward's recompute skips the L x L attention forward — the
 # kernels are deterministic, so the recomputed and the kept tensors are bit-identical.  The budget
-# is per training step: the trainer calls reset_attn_stash() at the start of every SFT / reward /
-# PAVRM step, so the generator's and the reward model's forwards of one step share it and the
-# stash never exceeds the budget.  0 (the default) keeps the pure checkpoint.  Under an external
-# torch.utils.checkpoint leave it at 0: that recompute would see a different keep decision.
+# bounds the bytes kept at any time: a forward takes `need` from it, the block's backward gives
+# it back (custom_ops._wan_block_bwd), so any training loop — the reference drivers included —
+# keeps using it step after step.  The trainers also reset it at the start of every step (a
+# graph dropped without a backward never gives its bytes back).  0 (the default) keeps the pure
+# checkpoint.  A block under an external torch.utils.checkpoint (apply_fsdp_checkpointing with
+# wrap_fused) has `stash_attn` off: that recompute could otherwise decide differently.
 _STASH = {"budget": 0, "left": 0}
 
 
@@ -53,6 +55,14 @@ def set_attn_stash_budget(nbytes):
 
 def reset_attn_stash():
     _STASH["left"] = _STASH["budget"]
+
+
+def stash_bytes(ao, lse):
+    return ao.numel() * ao.element_size() + lse.numel() * lse.element_size()
+
+
+def credit_attn_stash(nbytes):
+    _STASH["left"] = min(_STASH["budget"], _STASH["left"] + int(nbytes))
 
 
 class Meta:
@@ -314,7 +324,7 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     return dx, torch.stack(de), dctx
 
 
-def block_apply(P, x, e, context, meta):
+def block_apply(P, x, e, context, meta, allow_keep=True):
     """The fused, checkpointed block through the `prfl::wan_block` custom op (its backward is
     `prfl::wan_block_backward`).  P: name -> fp32 parameter (the block's, without
     'modulation'); x [B, L, C], e [B, 6, C] fp32 (modulation + e0), context [B, Lc, C] bf16.
@@ -328,7 +338,7 @@ def block_apply(P, x, e, context, meta):
     records = torch.is_grad_enabled() and (x.requires_grad or e.requires_grad or
                                            context.requires_grad or
                                            any(p.requires_grad for p in params))
-    keep = records and _STASH["left"] >= need
+    keep = allow_keep and records and _STASH["left"] >= need
     if keep:
         _STASH["left"] -= need
     grid = [int(v) for g in meta.grid for v in g]

@@ -130,6 +130,8 @@ def _wan_block_bwd(ctx, dout, _dao, _dlse):
     x, e, context, rope_tab, ao, lse, *params = ctx.saved_tensors
     nh, grid, seq_lens, i2v, eps, fp8 = ctx.args
     rx, re, rc, rp = ctx.req
+    if ao.numel():                      # the kept (ao, lse) die with this node (block.py)
+        B.credit_attn_stash(B.stash_bytes(ao, lse))
     if dout is None:
         return (None,) * 3 + ([None] * len(params),) + (None,) * 8
     res = wan_block_backward(dout.contiguous(), x, e, context, params, ao, lse, nh, grid,

@@ -38,6 +38,9 @@ class GradReducer:
         self.small_pending = []
         self.backend = dist.get_backend() if on else None
         self.handles = []
+        self.time_tail = False      # bench.py: HIP-event time of the exposed all-reduce tail
+        self.tail_ms = []
+        self._tail_ev = []
         if on:
             for p in self.params:
                 self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
@@ -67,6 +70,10 @@ class GradReducer:
 
     def end(self):
         """Call after loss.backward(): completes the exchange."""
+        ev0 = None
+        if self.active and self.time_tail and torch.cuda.is_available():
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()                 # the backward's last kernel on the compute stream
         if self.active:
             self._flush_small()
             for w, payload in self.works:
@@ -83,6 +90,20 @@ class GradReducer:
                 elif self.backend != "nccl":
                     payload[0].div_(self.world)
             self.works = []
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()                 # the stream has waited for every reduce of this backward
+            self._tail_ev.append((ev0, ev1))
+
+    def collect_tail_ms(self):
+        """Exposed all-reduce tail of each timed backward (ms), then reset."""
+        out = []
+        for a, b in self._tail_ev:
+            b.synchronize()
+            out.append(a.elapsed_time(b))
+        self._tail_ev = []
+        self.tail_ms = out
+        return out
 
 
 def broadcast_int(v, src=0, device="cpu"):
@@ -92,6 +113,14 @@ def broadcast_int(v, src=0, device="cpu"):
     t = torch.tensor([int(v)], dtype=torch.long, device=device)
     dist.broadcast(t, src=src)
     return int(t.item())
+
+
+def all_reduce_max(t):
+    if not is_dist():
+        return t
+    t = t.clone()
+    dist.all_reduce(t, dist.ReduceOp.MAX)
+    return t
 
 
 def all_reduce_mean(t):

@@ -53,7 +53,11 @@ def apply_fsdp_checkpointing(model, no_split_modules, p=1, wrap_fused=False):
             block_idx += 1
             if block_idx * p >= cut_off:
                 cut_off += 1
-                return wrap_fused or not getattr(submodule, "self_checkpointing", False)
+                fused = getattr(submodule, "self_checkpointing", False)
+                if fused and wrap_fused:
+                    # the wrapper's recompute must see the same (empty) attention stash
+                    submodule.stash_attn = False
+                return wrap_fused or not fused
         return False
 
     apply_activation_checkpointing(model, checkpoint_wrapper_fn=non_reentrant_wrapper,

@@ -177,6 +177,7 @@ class WanAttentionBlock(nn.Module):
 
     fp8_gemm = False    # config C5's fp8 path (WanModel.set_fp8_gemm); the reference is bf16-only
     self_checkpointing = True   # forward is already the per-block checkpoint (fsdp_utils.py)
+    stash_attn = True           # may keep its attention output for the backward (block.py)
 
     def __init__(self, cross_attn_type, dim, ffn_dim, num_heads, window_size=(-1, -1),
                  qk_norm=True, cross_attn_norm=False, eps=1e-6):
@@ -216,7 +217,8 @@ class WanAttentionBlock(nn.Module):
                           [int(s) for s in seq_lens.tolist()], _rope_table(freqs, x.device),
                           self.i2v, self.eps, fp8=self.fp8_gemm)
             ctx = context if context.dtype == torch.bfloat16 else context.to(torch.bfloat16)
-            return B.block_apply(P, x.contiguous(), em.contiguous(), ctx.contiguous(), meta)
+            return B.block_apply(P, x.contiguous(), em.contiguous(), ctx.contiguous(), meta,
+                                 allow_keep=self.stash_attn)
 
 
 class Head(nn.Module):

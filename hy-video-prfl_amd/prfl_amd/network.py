@@ -60,6 +60,10 @@ class QueryAttention(nn.Module):
             x = x.reshape(sp * bs, L, E)
         elif x.dim() != 3:
             raise ValueError(f"Unsupported input shape: {tuple(x.shape)}")
+        if self.training and self.dropout > 0:
+            # nn.MultiheadAttention applies attention dropout in training mode; the query_pool
+            # kernel has none (every shipped config sets dropout 0 or runs the head in eval)
+            raise NotImplementedError("QueryAttention: attention dropout > 0 in training mode")
         n = x.shape[0]
         queries = self.queries.unsqueeze(0).expand(n, -1, -1)
         if e is not None:

@@ -326,6 +326,16 @@ def prof_collect():
     return {k: dict(count=counts[i], ms=ms[i], work=work[i]) for k, i in _lib.KID.items()}
 
 
+def prof_clock():
+    """Effective shader clock of the self-attention forwards since the last call (MHz)."""
+    import ctypes
+    v = (ctypes.c_double * 3)()
+    n = ctypes.c_int64()
+    base = ctypes.addressof(v)
+    call("prfl_prof_clock", P(base), P(base + 8), P(base + 16), P(ctypes.addressof(n)))
+    return dict(mean_mhz=v[0], min_mhz=v[1], max_mhz=v[2], launches=n.value)
+
+
 def _coef_array(coef):
     import ctypes
     assert len(coef) == 11

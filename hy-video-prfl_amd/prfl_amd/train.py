@@ -8,7 +8,12 @@ Restates the per-iteration logic of the reference drivers (which cannot travel t
   * ``pavrm_step``   — `scripts/pavrm/train_pavrm.py:671-920` (BCE reward-model training)
   * ``build_lrm``    — `train_prfl.py:217-266` (first `trainable_blocks` of a Wan model, no head)
 Optimizer semantics kept: loss / gradient_accumulation_steps, clip_grad_norm_(1.0) on the
-accumulated grads every micro-step, optimizer.step() when (step+1) % accum == 0 in BOTH steps.
+accumulated grads every micro-step, optimizer.step() when (step+1) % accum == 0 in BOTH steps
+(the reward step's gradient accumulates onto the SFT step's: no zero_grad between them).
+Failure handling kept (`train_prfl.py:800-811`, `train_pavrm.py:874-880`): a NaN / Inf loss skips
+the backward and the optimizer step and reports loss 0 / grad_norm 0; |loss| > 1e6 is clamped
+(zero gradient).  Under data parallelism the skip is agreed across ranks (one MAX all-reduce of
+the flag): a rank that skipped alone would leave the others waiting in the gradient all-reduce.
 """
 import random
 
@@ -17,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import block as _block
-from .dist import GradReducer, all_reduce_mean, broadcast_int
+from .dist import GradReducer, all_reduce_max, all_reduce_mean, broadcast_int, is_dist
 from .network import forward_mlp
 from .optim import AdamW, clip_grad_norm_
 from .schedulers import FlowMatchDiscreteScheduler, FlowUniPCMultistepScheduler
@@ -42,6 +47,22 @@ def build_lrm(model, trainable_blocks=range(8)):
     for p in model.parameters():
         p.requires_grad_(False)
     return model
+
+
+def guard_loss(loss):
+    """`train_prfl.py:800-811` / `train_pavrm.py:874-880`: None for a NaN / Inf loss (the caller
+    skips backward and optimizer step), the loss clamped to [-1e6, 1e6] when |loss| > 1e6 (whose
+    gradient is then zero, as torch.clamp's), else the loss unchanged.  One host read of the
+    flags, as the reference's `loss.item()`; the NaN flag is the MAX over data-parallel ranks."""
+    d = loss.detach().float()
+    bad, big = (bool(v) for v in torch.stack([~torch.isfinite(d), d.abs() > 1e6]).tolist())
+    if is_dist():
+        bad = bool(all_reduce_max(torch.tensor([float(bad)], device=d.device)).item())
+    if bad:
+        return None
+    if big:                                  # the clamp itself stays per rank, as the reference's
+        return torch.clamp(loss, -1e6, 1e6)
+    return loss
 
 
 class PRFLTrainer:
@@ -71,6 +92,9 @@ class PRFLTrainer:
         self.unipc = FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
                                                  use_dynamic_shifting=False)
 
+    def _guard(self, loss):
+        return guard_loss(loss)
+
     def _backward_and_step(self, loss, step):
         self.reducer.begin()
         loss.backward()
@@ -86,14 +110,20 @@ class PRFLTrainer:
                     y=batch2list(cond) if cond is not None else None)
 
     def sft_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
-                 generator=None):
-        """train_prfl.py:900-980."""
+                 generator=None, noise=None, timestep=None):
+        """train_prfl.py:900-980.  `noise` / `timestep` (a value of the 1000-step schedule's
+        `timesteps`) replace the random draws when given."""
         _block.reset_attn_stash()
         bsz = latents.shape[0]
-        noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
-                            device=latents.device)
-        timestep, sigma = self.fm.get_train_timestep_and_sigma(
-            weighting_scheme="uniform", batch_size=bsz, device=latents.device, n_dim=latents.ndim)
+        if noise is None:
+            noise = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                                device=latents.device)
+        if timestep is None:
+            timestep, sigma = self.fm.get_train_timestep_and_sigma(
+                weighting_scheme="uniform", batch_size=bsz, device=latents.device,
+                n_dim=latents.ndim)
+        else:
+            sigma = self.fm.get_train_sigma(timestep, n_dim=latents.ndim, device=latents.device)
         noisy = self.fm.add_noise(latents, noise, sigma)
         pred = list2batch(self.transformer(x=batch2list(noisy), t=timestep,
                                            **self._kw(noisy, text_states, seq_len, image_embeds,
@@ -104,15 +134,19 @@ class PRFLTrainer:
         return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm)
 
     def reward_step(self, step, latents, text_states, seq_len, image_embeds=None, cond=None,
-                    mid_timestep=None, generator=None):
-        """train_prfl.py:585-846."""
+                    mid_timestep=None, generator=None, noise=None):
+        """train_prfl.py:585-846.  `noise` replaces the initial latent's random draw
+        (`randn_like(latents)`, `:637`) when given."""
         _block.reset_attn_stash()
         sch = self.unipc
         sch.set_timesteps(num_inference_steps=self.inference_steps, device=latents.device,
                           shift=self.flow_shift)
         timesteps = sch.timesteps
-        latent = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
-                             device=latents.device)
+        if noise is None:
+            latent = torch.randn(latents.shape, generator=generator, dtype=latents.dtype,
+                                 device=latents.device)
+        else:
+            latent = noise.to(latents.dtype)
         if mid_timestep is None:
             mid_timestep = random.randint(0, self.inference_steps - 2)
         mid = broadcast_int(mid_timestep, device=latents.device)
@@ -134,6 +168,10 @@ class PRFLTrainer:
                                     **kw))
         reward = forward_mlp(self.mlp, self.qa(feats))
         loss = 0.1 * F.relu(-reward.squeeze() + 2).mean()
+        loss = self._guard(loss)                                       # :800-811
+        if loss is None:
+            return dict(loss=torch.tensor(0.0), grad_norm=0, mid=mid, reward=reward.detach(),
+                        skipped=True)
         loss = loss / self.grad_accum
         grad_norm = self._backward_and_step(loss, step)
         return dict(loss=all_reduce_mean(loss.detach().float()), grad_norm=grad_norm, mid=mid,
@@ -195,6 +233,9 @@ class PAVRMTrainer:
                                     output_features=True, selected_layers=self.feature_layer))
         out = forward_mlp(self.mlp, self.qa(feats))
         loss = F.binary_cross_entropy(out.squeeze().float(), label.squeeze().float())
+        loss = guard_loss(loss)                                        # train_pavrm.py:874-880
+        if loss is None:
+            return dict(loss=torch.tensor(0.0), grad_norm=0, prob=out.detach(), skipped=True)
         self.reducer.begin()
         loss.backward()
         self.reducer.end()

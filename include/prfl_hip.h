@@ -206,6 +206,9 @@ int prfl_unipc_step_bwd(const void* grad_prev, float* grad_model_output, int64_t
 /* ---- profiling (bench.py roofline) -------------------------------------------------------- */
 int prfl_prof_enable(int on);
 int prfl_prof_collect(int64_t* counts, double* ms, double* work, int nkid);
+/* effective shader clock (MHz: launch-time-weighted mean, min, max; n = launches) of the
+ * self-attention forwards since the last call, from s_memtime / s_memrealtime in workgroup 0 */
+int prfl_prof_clock(double* mean_mhz, double* min_mhz, double* max_mhz, int64_t* n);
 
 #ifdef __cplusplus
 }

@@ -350,6 +350,145 @@ def case_toy_pavrm():
     save("toy_pavrm", **out)
 
 
+def _summ(tensors, head=1024, full_max=4096):
+    """Per-tensor summary of a {name: tensor} dict: full values for small tensors; for large ones
+    the first `head` values, the L2 norm and the projection onto a seeded random vector."""
+    out = {}
+    for n, g in tensors.items():
+        g = g.detach().float().flatten()
+        if g.numel() <= full_max:
+            out["full/" + n] = g.numpy()
+        else:
+            r = torch.from_numpy(seeded.randn("proj:" + n, (g.numel(),)))
+            out["head/" + n] = g[:head].numpy()
+            out["norm/" + n] = np.float64(g.double().norm().item())
+            out["proj/" + n] = np.float64((g.double() * r.double()).sum().item())
+    return out
+
+
+TRAINER_GA = 2.0          # gradient_accumulation_steps (the configs' 5.0, shortened to 2)
+TRAINER_LR = 5e-6         # train_prfl_t2v_480.yaml optimizer.learning_rate
+TRAINER_SFT_IDX = (613, 287)
+TRAINER_MID = (2, 1)
+
+
+def _trainer_run(truth):
+    """Two PRFL iterations (step 0, then step 1 = an optimizer-step boundary for
+    gradient_accumulation_steps 2) restating `train_prfl.py` on the reference modules:
+    `train_step` (`:900-980`: flow-matching SFT loss / GA, backward, `clip_grad_norm_(1.0)`,
+    AdamW step + zero_grad when (step+1) % GA == 0) then `train_step_refl` (`:585-846`: UniPC
+    rollout to `mid`, grad-enabled generator step, differentiable UniPC step, frozen 1-block LRM
+    + QueryAttention + MLP, hinge, NaN/Inf check and clamp `:800-811`, loss / GA, backward onto
+    the SFT step's accumulated grads, clip, AdamW step at the boundary).  AdamW = `optimizer_init`
+    (`:479-491`: all generator parameters, lr 5e-6, betas (0.9, 0.999), wd 0.01, eps 1e-8).
+    `truth`: the same run in fp32 without autocast, with unrounded attention and fp32 latents:
+    the values the bf16 runs approximate.  Records per backward the fresh gradient increment,
+    the clipped norm, the losses, and each optimizer step's parameter update."""
+    ac = dict(AC, enabled=not truth)
+    saved = M.flash_attention
+    if truth:
+        M.flash_attention = _exact_attention
+    try:
+        gen = _toy_model("t2v")
+        lrm = _toy_model("t2v")
+        lrm.blocks = torch.nn.ModuleList([lrm.blocks[0]])
+        del lrm.head
+        lrm.head = None
+        for p in lrm.parameters():
+            p.requires_grad_(False)
+        qa = load_seeded(NET.QueryAttention(256, 1, 8, 0., return_type="query"), prefix="tqa.")
+        mlp = load_seeded(NET.MLP(256), prefix="tmlp.")
+        for p in list(qa.parameters()) + list(mlp.parameters()):
+            p.requires_grad_(False)
+        params = [p for p in gen.parameters() if p.requires_grad]
+        named = {n: p for n, p in gen.named_parameters() if p.requires_grad}
+        opt = torch.optim.AdamW(params, lr=TRAINER_LR, betas=(0.9, 0.999), weight_decay=0.01,
+                                eps=1e-8)
+        fm = FM.FlowMatchDiscreteScheduler(shift=5.0)
+        fm.set_timesteps(1000, dtype=torch.int64)
+        sch = UNIPC.FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                                use_dynamic_shifting=False)
+        lat_dt = torch.float32 if truth else torch.bfloat16
+        ctx = torch.from_numpy(seeded.randn("trainer.ctx", (1, 20, TOY["text_dim"]))) \
+            .to(torch.bfloat16).to(lat_dt)
+        x0 = torch.from_numpy(seeded.randn("trainer.x0", (1,) + TOY_LATENT)).to(torch.bfloat16) \
+            .to(lat_dt)
+        L = 105
+        out = {}
+
+        def backward_and_step(loss, step, tag):
+            before = {n: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p))
+                      for n, p in named.items()}
+            loss.backward()
+            fresh = {n: p.grad.detach() - before[n] for n, p in named.items()}
+            out.update({f"{tag}:fresh:" + k: v for k, v in _summ(fresh).items()})
+            gn = torch.nn.utils.clip_grad_norm_(params, max_norm=1.0)
+            out[f"{tag}:grad_norm"] = np.float64(gn.item())
+            if (step + 1) % TRAINER_GA == 0:
+                p0 = {n: p.detach().clone() for n, p in named.items()}
+                opt.step()
+                opt.zero_grad()
+                upd = {n: p.detach() - p0[n] for n, p in named.items()}
+                out.update({f"{tag}:upd:" + k: v for k, v in _summ(upd).items()})
+
+        for step in (0, 1):
+            # ---- train_step (SFT) ----
+            noise = torch.from_numpy(seeded.randn(f"trainer.sft_noise.{step}", (1,) + TOY_LATENT)) \
+                .to(torch.bfloat16).to(lat_dt)
+            idx = TRAINER_SFT_IDX[step]
+            timestep = fm.timesteps[[idx]]
+            sigma = fm.sigmas[[idx]].float().view(1, 1, 1, 1, 1)
+            noisy = fm.add_noise(x0, noise, sigma)
+            with torch.autocast(**ac):
+                pred = DU.list2batch(gen(x=DU.batch2list(noisy), t=timestep,
+                                         context=DU.batch2list(ctx), seq_len=L))
+            target = fm.get_train_target(x0, noise)
+            weighting = fm.get_train_loss_weighting(sigma)
+            loss = torch.mean(weighting.float() * (pred.float() - target.float()) ** 2)
+            loss = loss / TRAINER_GA
+            out[f"it{step}:sft:loss"] = np.float64(loss.item())
+            backward_and_step(loss, step, f"it{step}:sft")
+            # ---- train_step_refl (reward) ----
+            sch.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
+            ts = sch.timesteps
+            latent = torch.from_numpy(seeded.randn(f"trainer.rwd_noise.{step}", (1,) + TOY_LATENT)) \
+                .to(torch.bfloat16).to(lat_dt)
+            mid = TRAINER_MID[step]
+            with torch.no_grad():
+                for i in range(mid):
+                    with torch.autocast(**ac):
+                        npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[i]]),
+                                                  context=DU.batch2list(ctx), seq_len=L))
+                        latent = sch.step(npred, ts[i], latent, return_dict=False)[0]
+            with torch.autocast(**ac):
+                npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[mid]]),
+                                          context=DU.batch2list(ctx), seq_len=L))
+            latent = sch.step(npred, ts[mid], latent, return_dict=False)[0]
+            with torch.autocast(**ac):
+                feats = DU.list2batch(lrm(x=DU.batch2list(latent), t=torch.tensor([ts[mid + 1]]),
+                                          context=DU.batch2list(ctx), seq_len=L,
+                                          output_features=True, selected_layers=[1]))
+                r = NET.forward_mlp(mlp, qa(feats))
+                loss = 0.1 * torch.relu(-r.squeeze() + 2).mean()
+                assert torch.isfinite(loss) and abs(loss.item()) <= 1e6
+            out[f"it{step}:rwd:reward"] = np.float64(r.item())
+            loss = loss / TRAINER_GA
+            out[f"it{step}:rwd:loss"] = np.float64(loss.item())
+            backward_and_step(loss, step, f"it{step}:rwd")
+        return out
+    finally:
+        M.flash_attention = saved
+
+
+def case_toy_prfl_trainer():
+    """PRFLTrainer parity: the reference run and its fp32 truth."""
+    ref = _trainer_run(truth=False)
+    t32 = _trainer_run(truth=True)
+    save("toy_prfl_trainer", ga=np.float64(TRAINER_GA), lr=np.float64(TRAINER_LR),
+         sft_idx=np.asarray(TRAINER_SFT_IDX), mid=np.asarray(TRAINER_MID), **ref,
+         **{"t32:" + k: v for k, v in t32.items()})
+
+
 def _exact_attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=None,
                      q_scale=None, causal=False, window_size=(-1, -1), deterministic=False,
                      dtype=None, version=None):
@@ -398,7 +537,9 @@ def _toy_pavrm_fp32_truth(step, states, noisy, timestep, ctx, label):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl", "pavrm"]
+    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl", "pavrm", "trainer"]
+    if "trainer" in which:
+        case_toy_prfl_trainer()
     if "pavrm" in which:
         case_toy_pavrm()
     if "ops" in which:

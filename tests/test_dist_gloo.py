@@ -183,3 +183,36 @@ def test_grad_reducer_rccl_branch_arithmetic_world2():
     for n, p in model.named_parameters():
         assert torch.allclose(g0[n], p.grad, atol=1e-6, rtol=1e-5), n
         assert torch.equal(g0[n], g1[n]), n
+
+
+def _guard_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from prfl_amd.train import guard_loss
+    res = []
+    # only rank 1's loss is NaN: both ranks skip (a lone skip would stall the grad all-reduce)
+    res.append(guard_loss(torch.tensor(float("nan") if rank == 1 else 0.5)) is None)
+    # both finite: neither skips; a large loss is clamped on its own rank only
+    big = guard_loss(torch.tensor(3e6 if rank == 0 else 0.25))
+    res.append(float(big))
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_nan_loss_skip_is_agreed_across_ranks_world2():
+    """`train_prfl.py:800-811` under data parallelism: the NaN / Inf skip is taken by every rank
+    when any rank's loss is bad; the |loss| > 1e6 clamp stays per rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, r0), (_, r1) = res
+    assert r0[0] and r1[0]
+    assert r0[1] == 1e6 and r1[1] == 0.25

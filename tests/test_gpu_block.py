@@ -170,8 +170,43 @@ def test_attention_stash_is_bit_identical(L, grid):
             xd = x.to(DEV).requires_grad_(True)
             meta = B.Meta(nh, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), False)
             out = B.block_apply(Pd, xd, e.to(DEV), ctx.to(DEV), meta)
+            if budget:          # the forward took its stash from the budget ...
+                assert B._STASH["left"] == budget - (L * dim * 2 + nh * L * 4)
             (out * up.to(DEV)).sum().backward()
+            # ... and the backward gave it back (no trainer reset needed between steps)
+            assert B._STASH["left"] == budget
             res.append([out.detach(), xd.grad] + [p.grad for p in Pd.values()])
     finally:
         B.set_attn_stash_budget(0)
     assert all(torch.equal(a, b) for a, b in zip(*res))
+
+
+def test_c1_block_forward_480p49f_vs_oracle():
+    """Config C1 (`pre_480`): one 14B WanAttentionBlock forward at 480p x 49f — L = 20 280
+    tokens, grid 13 x 30 x 52 (SURVEY §8 geometry), inputs as SURVEY §8d C1 (x ~ N(0,1) fp32,
+    e0 ~ 0.1 N(0,1), 512 text tokens ~ N(0,1)).  The oracle computes 1 024 output rows spread over
+    the sequence (first / last rows included) with keys and values from all 20 280 tokens
+    (wan_oracle.block_forward(rows=...)); block output rel-L2 <= 1e-2."""
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    torch.set_num_threads(16)
+    P = seeded_params(block_shapes("blocks.0.", 5120, 13824, False), prefix="c1.")
+    grid = (13, 30, 52)
+    L = 13 * 30 * 52
+    g = torch.Generator().manual_seed(20280)
+    x = torch.randn(1, L, 5120, generator=g)
+    e = torch.randn(1, 6, 5120, generator=g) * 0.1
+    ctx = torch.randn(1, 512, 5120, generator=g).to(torch.bfloat16)
+    names = B.param_names(False)
+    Pd = {n: P["blocks.0." + n].to(DEV) for n in names}
+    meta = B.Meta(40, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), False)
+    with torch.no_grad():
+        out = B.block_apply(Pd, x.to(DEV), (P["blocks.0.modulation"] + e).to(DEV), ctx.to(DEV),
+                            meta).cpu()
+    rows = torch.cat([torch.arange(0, 16), torch.linspace(16, L - 17, 992).long(),
+                      torch.arange(L - 16, L)])
+    with torch.no_grad():
+        ref = O.block_forward(P, "blocks.0.", x, e, torch.tensor([grid]), O.rope_freqs(128),
+                              ctx.float(), 40, seq_len=L, rows=rows)
+    assert torch.isfinite(out).all()
+    assert rel(out[:, rows], ref) < 1e-2, rel(out[:, rows], ref)

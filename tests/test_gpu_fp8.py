@@ -3,8 +3,11 @@ block-scaled fp8 MFMA GEMM (csrc/gemm.hip) on the MI355X.
 
 Bars: quantisation bit-exact vs torch's float8_e4m3fn cast of the same scaled values; the GEMM
 exact on integer data (every product and partial sum representable) and within fp32 summation
-order + the bf16 output rounding (rel-L2 <= 3e-3) on random data; an fp8 linear against the
-bf16 linear of the same operands within the SURVEY §8c fp8 tolerance (rel-L2 <= 5e-2)."""
+order + the bf16 output rounding (rel-L2 <= 3e-3) on random data, including every 720p x 81f
+projection shape of the block (M = 73 920); an fp8 linear against the bf16 linear of the same
+operands within the SURVEY §8c fp8 tolerance (rel-L2 <= 5e-2); the real-width I2V block on the
+fp8 path at L = 4 200 against the oracle's fp32 truth, held to k = 8 times the bf16 path's
+error against that same truth (see test_block_fp8_vs_fp32_truth)."""
 import pytest
 import torch
 
@@ -84,43 +87,129 @@ def test_gemm_fp8_random_epilogues(M, N, K):
     assert rel(y.float(), yb.float()) < 5e-2
 
 
-@pytest.mark.parametrize("i2v", [False, True])
-def test_block_fp8_path_vs_bf16_path(i2v):
-    """Real-width (C=5120, 40 heads, F=13824) fused block, L = 1536: the fp8 path's residual
-    update and gradients against the bf16 path's (<= 8e-2: two chained fp8 GEMMs per branch)."""
+def _rel_gpu(a, b, rows=8192):
+    """rel-L2 of two large [M, N] device tensors, reduced on the device in fp64 row blocks."""
+    num = torch.zeros((), dtype=torch.float64, device=a.device)
+    den = torch.zeros((), dtype=torch.float64, device=a.device)
+    for i in range(0, a.shape[0], rows):
+        x, y = a[i:i + rows].double(), b[i:i + rows].double()
+        num += (x - y).pow(2).sum()
+        den += y.pow(2).sum()
+        del x, y
+    return (num.sqrt() / den.sqrt()).item()
+
+
+@pytest.mark.parametrize("N,K", [(15360, 5120), (5120, 5120), (13824, 5120), (5120, 13824)])
+def test_gemm_fp8_720p_shapes(N, K):
+    """The fp8 GEMM at every 720p x 81f forward-projection shape of config C5 (M = 73 920 tokens;
+    fused QKV 15360 x 5120, O / cross q / cross o 5120 x 5120, FFN in 13824 x 5120, FFN out
+    5120 x 13824) against the product of the dequantised operands computed in fp32 on the same
+    device (torch.matmul, allow_tf32 off): within fp32 summation order + the bf16 output rounding."""
+    from prfl_amd import ops
+    assert not torch.backends.cuda.matmul.allow_tf32
+    M = 73920
+    g = torch.Generator(device=DEV).manual_seed(N + K)
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, generator=g, device=DEV) / K ** 0.5
+    bias = (0.1 * torch.randn(N, generator=g, device=DEV)).to(torch.bfloat16)
+    xq, xs = ops.quant_rows_fp8(x)
+    del x
+    wq, ws = ops.quant_rows_fp8(w)
+    y = ops.linear_fp8(xq, xs, wq, ws, bias)
+    torch.cuda.synchronize()
+    wd = (wq.float() * ws[:, None]).T.contiguous()
+    ref = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    for i in range(0, M, 16384):        # dequantised A rows in blocks (fp32 A would be 4 GB)
+        a = xq[i:i + 16384].float() * xs[i:i + 16384, None]
+        torch.matmul(a, wd, out=ref[i:i + 16384])
+        ref[i:i + 16384] += bias.float()
+        del a
+    r = _rel_gpu(y, ref.to(torch.bfloat16))
+    assert r < 3e-3, r
+    assert torch.isfinite(y).all()
+
+
+def _block_update(P, names, x, e, ctx, grid, up, i2v, fp8):
+    from oracle import wan_oracle as O
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    L = x.shape[1]
+    Pd = {n: P["b." + n].to(DEV).requires_grad_(True) for n in names}
+    xd = x.to(DEV).requires_grad_(True)
+    meta = B.Meta(40, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), i2v, fp8=fp8)
+    out = B.block_apply(Pd, xd, e.to(DEV), ctx.to(DEV), meta)
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    return ((out.detach() - xd.detach()).cpu(), xd.grad.cpu(),
+            {n: p.grad.cpu() for n, p in Pd.items()})
+
+
+def test_block_fp8_vs_fp32_truth():
+    """Config C5's fp8 path on the real-width I2V block (C = 5120, 40 heads, F = 13 824, 257
+    image + 512 text context tokens) at L = 4 200 (3 x 35 x 40: the production long-KV attention
+    kernels), against the oracle.
+
+    Reference points, all on the same weights and inputs: the oracle with the reference's bf16
+    cast points (`wan_oracle.block_forward`, = the reference under autocast) and the oracle's
+    fp32 TRUTH (every cast point removed: fp32 operands everywhere, unrounded attention).
+    Criterion: err(fp8 path vs truth) <= k * err(bf16 path vs truth), k = 8, for
+    the block's residual update, the input gradient and the projection-weight gradients.
+    Why k = 8: e4m3 keeps 3 mantissa bits to bf16's 7, a unit roundoff 2^-4 vs 2^-8 (16x) on
+    both operands of the six forward projections; everything else (LN / RMSNorm / softmax / the
+    residual stream / the backward GEMMs) is computed as on the bf16 path, so the block error
+    grows by less than the per-rounding ratio — 8 = half of it leaves headroom for the two
+    chained fp8 GEMMs per branch without admitting a broken kernel (a wrong scale or a lost
+    k-block is >= 100 % off).  The bf16 path itself is also held to the oracle (<= 1e-2)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
     from shapes import block_shapes, seeded_params
     from oracle import wan_oracle as O
     from prfl_amd import block as B
-    from prfl_amd import ops
-    C, Fd, nh = 5120, 13824, 40
-    P = seeded_params(block_shapes("b.", C, Fd, i2v), prefix="fp8b.")
+    torch.set_num_threads(16)
+    C, Fd, nh, i2v = 5120, 13824, 40, True
+    P = seeded_params(block_shapes("b.", C, Fd, i2v), prefix="fp8t.")
     names = B.param_names(i2v)
-    grid = (2, 24, 32)
+    grid = (3, 35, 40)
     L = grid[0] * grid[1] * grid[2]
-    g = torch.Generator().manual_seed(5)
+    g = torch.Generator().manual_seed(11)
     x = torch.randn(1, L, C, generator=g)
-    e = torch.randn(1, 6, C, generator=g) * 0.1 + P["b.modulation"]
-    ctx = torch.randn(1, 512 + (257 if i2v else 0), C, generator=g).to(torch.bfloat16)
+    e0 = torch.randn(1, 6, C, generator=g) * 0.1
+    e = e0 + P["b.modulation"]
+    ctx = torch.randn(1, 512 + 257, C, generator=g).to(torch.bfloat16)
     up = torch.randn(1, L, C, generator=g)
-    res = {}
-    for fp8 in (False, True):
-        Pd = {n: P["b." + n].to(DEV).requires_grad_(True) for n in names}
-        xd = x.to(DEV).requires_grad_(True)
-        meta = B.Meta(nh, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), i2v, fp8=fp8)
-        out = B.block_apply(Pd, xd, e.to(DEV), ctx.to(DEV), meta)
-        (out * up.to(DEV)).sum().backward()
-        res[fp8] = (out.detach() - xd.detach(), xd.grad, {n: p.grad for n, p in Pd.items()})
-    (d0, gx0, G0), (d1, gx1, G1) = res[False], res[True]
-    r = {"update": rel(d1, d0), "dx": rel(gx1, gx0)}
-    for n in ("self_attn.q.weight", "self_attn.o.weight", "ffn.0.weight", "ffn.2.weight",
-              "cross_attn.q.weight"):
-        r[n] = rel(G1[n], G0[n])
-    print("fp8 vs bf16 block rel-L2:", {k: round(v, 4) for k, v in r.items()})
-    # One e4m3 GEMM (3 mantissa bits on both operands) is ~3.5-4 % rel-L2 from its bf16 twin
-    # (test above, held to SURVEY §8c's 5e-2); a block chains two in series on each branch
-    # (QKV -> attention -> O, FFN in -> GELU -> FFN out), measured 5.2 % on its update.
-    for k, v in r.items():
-        assert v < 8e-2, (k, v)
+    hip = {fp8: _block_update(P, names, x, e, ctx, grid, up, i2v, fp8) for fp8 in (False, True)}
+
+    def oracle(truth):
+        saved = O.bf
+        if truth:
+            O.bf = lambda t: t
+        try:
+            Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+            xr = x.clone().requires_grad_(True)
+            ref = O.block_forward(Pr, "b.", xr, e0, torch.tensor([grid]), O.rope_freqs(128),
+                                  ctx.float(), nh, seq_len=L, i2v=i2v)
+            (ref * up).sum().backward()
+            return ((ref - x).detach(), xr.grad, {n: Pr["b." + n].grad for n in names})
+        finally:
+            O.bf = saved
+    truth = oracle(True)
+    ref16 = oracle(False)
+    keys = ["update", "dx", "self_attn.q.weight", "self_attn.o.weight", "cross_attn.q.weight",
+            "cross_attn.o.weight", "ffn.0.weight", "ffn.2.weight"]
+
+    def errs(res, against):
+        d, gx, G = res
+        td, tgx, tG = against
+        out = {"update": rel(d, td), "dx": rel(gx, tgx)}
+        out.update({n: rel(G[n], tG[n]) for n in keys[2:]})
+        return out
+    e16, e8, eor = errs(hip[False], truth), errs(hip[True], truth), errs(ref16, truth)
+    e16_vs_oracle = errs(hip[False], ref16)
+    print("vs truth: bf16 path", {k: round(v, 4) for k, v in e16.items()})
+    print("vs truth: fp8 path ", {k: round(v, 4) for k, v in e8.items()})
+    print("vs truth: oracle   ", {k: round(v, 4) for k, v in eor.items()})
+    print("fp8 / bf16 ratio   ", {k: round(e8[k] / e16[k], 2) for k in keys})
+    for k in keys:
+        assert e8[k] <= 8 * e16[k], (k, e8[k], e16[k])
+    assert e16_vs_oracle["update"] < 1e-2 and e16_vs_oracle["dx"] < 3e-2, e16_vs_oracle

@@ -133,3 +133,44 @@ def test_720p_data_parallel_memory_plan_fits():
     assert runs
     alloc, res = mp.from_measurement(8, 20.0, runs[-1])
     assert res < mp.CARD_GB - 20, (runs[-1], alloc, res)
+
+
+def test_external_checkpoint_turns_the_attention_stash_off():
+    """apply_fsdp_checkpointing(wrap_fused=True) wraps the fused blocks in a second, external
+    non-reentrant checkpoint; its recompute must see the same keep decision as the original
+    forward, so those blocks never stash.  Unwrapped blocks keep it."""
+    from prfl_amd.fsdp_utils import apply_fsdp_checkpointing, get_no_split_modules
+    from prfl_amd.model import WanModel
+    for wrap in (False, True):
+        m = WanModel(model_type="t2v", in_dim=16, **TOY)
+        apply_fsdp_checkpointing(m, get_no_split_modules(m), p=1, wrap_fused=wrap)
+        blocks = [mod for mod in m.modules() if type(mod).__name__ == "WanAttentionBlock"]
+        assert len(blocks) == TOY["num_layers"]
+        assert all(b.stash_attn is (not wrap) for b in blocks)
+
+
+def test_query_attention_rejects_training_dropout():
+    """nn.MultiheadAttention applies attention dropout in training mode; the pooling kernel has
+    none, so QueryAttention refuses instead of silently differing."""
+    from prfl_amd.network import QueryAttention
+    qa = QueryAttention(64, 1, 8, dropout=0.1)
+    qa.train()
+    with pytest.raises(NotImplementedError):
+        qa(torch.zeros(1, 4, 64))
+
+
+def test_loss_guard_matches_reference_semantics():
+    """`train_prfl.py:800-811` (single process): NaN / Inf -> skip; |loss| > 1e6 -> clamp, whose
+    gradient is zero; otherwise the loss and its gradient pass unchanged."""
+    from prfl_amd.train import guard_loss
+    assert guard_loss(torch.tensor(float("nan"))) is None
+    assert guard_loss(torch.tensor(float("-inf"))) is None
+    x = torch.tensor(2.0, requires_grad=True)
+    big = guard_loss(x * 1e6)
+    assert float(big) == 1e6
+    big.backward()
+    assert float(x.grad) == 0.0
+    y = torch.tensor(0.3, requires_grad=True)
+    ok = guard_loss(y * 2)
+    ok.backward()
+    assert float(ok) == float(torch.tensor(0.3) * 2) and float(y.grad) == 2.0

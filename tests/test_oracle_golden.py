@@ -151,3 +151,28 @@ def test_flowmatch(golden):
     ts, sig = O.flowmatch_sigmas(1000, 5.0)
     assert np.array_equal(ts.numpy(), g["fm_timesteps"])
     assert np.allclose(sig.numpy(), g["fm_sigmas"], atol=1e-7)
+
+
+def test_oracle_row_subset_and_chunked_attention_match_full():
+    """The checker shortcuts used at C1's L = 20 280: block_forward(rows=...) equals the rows
+    of the full forward, and the no-grad chunked attention equals the autograd FA2 path."""
+    import torch
+    from oracle import wan_oracle as O
+    from shapes import block_shapes, seeded_params
+    P = seeded_params(block_shapes("b.", 256, 512), prefix="rows.")
+    g = torch.Generator().manual_seed(4)
+    L = 3 * 5 * 7 + 3
+    x = torch.randn(1, L, 256, generator=g)
+    e = torch.randn(1, 6, 256, generator=g) * 0.1
+    ctx = torch.randn(1, 512, 256, generator=g).to(torch.bfloat16).float()
+    grid, fr = torch.tensor([[3, 5, 7]]), O.rope_freqs(128)
+    with torch.no_grad():
+        full = O.block_forward(P, "b.", x, e, grid, fr, ctx, 2, seq_len=105)
+        rows = torch.tensor([0, 1, 50, 104, 105, L - 1])
+        sub = O.block_forward(P, "b.", x, e, grid, fr, ctx, 2, seq_len=105, rows=rows)
+    assert torch.allclose(sub, full[:, rows], rtol=1e-5, atol=1e-5)
+    q, k, v = (torch.randn(1, 70, 2, 128, generator=g) for _ in range(3))
+    with torch.no_grad():
+        a = O.attention(q, k, v, k_len=50, q_chunk=16)
+    b = O._FlashAttention.apply(q, k, v, 50, 128 ** -0.5)
+    assert (a - b).abs().max().item() <= 2 ** -8 * b.abs().max().item()
