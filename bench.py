@@ -327,6 +327,7 @@ def main():
             # (each rank holds and streams 1/N of them, then broadcasts the tensors it updated)
             big = args.workload.endswith("720") or args.toy
             tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
+                             feature_layer=(TOY_DIMS["lrm_layers"],) if args.toy else (8,),
                              optimizer_state_on_host=big or os.environ.get("PRFL_OPT_HOST") == "1",
                              optimizer_shard=big and world > 1,
                              optimizer_overlap=os.environ.get("PRFL_OPT_OVERLAP", "1") == "1")
@@ -348,7 +349,8 @@ def main():
             del gen
             for blk in lrm.blocks:
                 blk.requires_grad_(True)
-            tr = PAVRMTrainer(lrm, qa, mlp)
+            tr = PAVRMTrainer(lrm, qa, mlp,
+                              feature_layer=(TOY_DIMS["lrm_layers"],) if args.toy else (8,))
             label = torch.ones(1, device=dev)
 
             def one(step, mid=None):

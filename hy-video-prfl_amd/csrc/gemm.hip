@@ -750,6 +750,239 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     epilogue4w<EPI, false>(g, acc, mb, nb);
 }
 
+// ---------------------------------------- 256x256, four waves, MFMA 32x32x16 (gemm4x) -------
+// gemm4w_kernel's tile, 4-slot ring, DMA schedule and one barrier per 32-deep K-slice, with each
+// wave's 128x128 computed as 4 x 4 MFMA 32x32x16 tiles (32 MFMAs of 32 cycles per slice instead
+// of 64 of 16): an MFMA holds the SIMD's vector issue for 8 cycles either way, so the slice's
+// issue slots spent on MFMAs halve (512 -> 256 of 1024 cycles) and the eight LDS-DMA pieces
+// and sixteen fragment reads no longer compete with the matrix pipe for issue (MI355X guide,
+// constants table: vector-instruction issue cost).  Same operand bytes and LDS reads per MFMA
+// FLOP.  Outputs are not bit-identical to the 16x16x32 kernels: one 32x32x16 MFMA rounds its
+// accumulator after 16 products, a 16x16x32 one after 32.
+// K-major slice image: [256 rows][32 k], 64-B rows, 16-B chunk c of row r at c ^ ((r >> 2) & 3)
+// (every 16-lane quarter of a b128 read — 16 rows x one chunk column — lands on 16 distinct
+// 16-B bank groups).  MN-major: two [32 k][128] halves, 256-B rows, 64-B chunk ^ (k & 3) (the 32
+// lanes of a b64 transposed read — 4 k-rows x 32 columns — cover the 256-B bank window once).
+__device__ __forceinline__ int kc_pos32(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+
+template <bool KC>
+__device__ __forceinline__ uint32_t piece_off32(int64_t ld, int wid, int lane, int i) {
+  const int piece = wid * 4 + i;                       // 16 pieces of 1 KiB per operand
+  if (KC) {          // 16 rows x 64 B per piece: LDS slot (row, pos) <- global chunk pos ^ swz(row)
+    const int row = piece * 16 + (lane >> 2), pos = lane & 3;
+    return (uint32_t)(row * ld * 2) + ((pos ^ ((row >> 2) & 3)) << 4);
+  }
+  // half piece>>3, 4 k-rows x 256 B per piece: LDS byte pb of row kr <- column byte pb ^ 64 (kr & 3)
+  const int kr = (piece & 7) * 4 + (lane >> 4), pb = (lane & 15) << 4;
+  const int lc = (pb ^ ((kr & 3) << 6)) >> 1;
+  return (uint32_t)(kr * ld * 2) + (uint32_t)(((piece >> 3) * 128 + lc) * 2);
+}
+
+// MFMA 32x32x16 operand of k-step s (16 k) of a slice: lane l gets row `base + (l & 31)` at
+// k = 16 s + 8 (l >> 5) + 0..7 (the A and the B operand have the same form).
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag32(const char* lds, int base, int s, int lane) {
+  if (KC) return *(const bf16x8*)(lds + kc_pos32(base + (lane & 31), 2 * s + (lane >> 5)));
+  const char* h = lds + (base >> 7) * 8192;
+  const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+  const int cb = ((base & 127) + 16 * (g & 1) + 4 * p) * 2;
+  const int k0 = 16 * s + 8 * (g >> 1) + q, k1 = k0 + 4;
+  return cat8(lds_read_tr(h + k0 * 256 + (cb ^ ((k0 & 3) << 6))),
+              lds_read_tr(h + k1 * 256 + (cb ^ ((k1 & 3) << 6))));
+}
+
+// Epilogue of gemm4x: the 16 (row block i, column tile jj) pieces in turn, each 4 column vectors
+// (register group q of acc[i][jj]: columns 32 jj + 8 q + 0..3 of the lane's group, rows 32 i +
+// (lane & 31)); per piece the per-element inputs and the bias / gate of its columns are loaded one
+// piece ahead.  Same arithmetic, in the same order, as epilogue_tile.
+template <int EPI, bool IN_BF16>
+__device__ __forceinline__ void epilogue4x(const GemmArgs& g, const f32x16 (&acc)[4][4], int mb, int nb) {
+  constexpr bool HAS_IN = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_DGELU;
+  using InT = typename std::conditional<IN_BF16, bf16x4, f32x4>::type;
+  const void* src = EPI == EPI_F32 ? (const void*)g.C : EPI == EPI_DGELU ? (const void*)g.aux : g.res;
+  const int64_t lds_in = EPI == EPI_F32 ? g.ldc : EPI == EPI_DGELU ? g.ldaux : g.ldr;
+  const bool any_in = HAS_IN && (EPI != EPI_F32 || g.accumulate);
+  struct Piece { InT in[4]; f32x4 bias[4], gate[4]; };
+  auto load = [&](int b, Piece& p) {
+    const int m = mb + 32 * (b >> 2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = nb + 32 * (b & 3) + 8 * q;
+      p.in[q] = InT{};
+      p.bias[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      p.gate[q] = (f32x4){1.f, 1.f, 1.f, 1.f};
+      if (n >= g.N) continue;
+      if (EPI != EPI_F32 && EPI != EPI_DGELU && g.bias) {
+        const bf16x4 bb = *(const bf16x4*)(g.bias + n);
+        p.bias[q] = (f32x4){bf2f(bb[0]), bf2f(bb[1]), bf2f(bb[2]), bf2f(bb[3])};
+      }
+      if (EPI == EPI_RESID && g.gate) p.gate[q] = *(const f32x4*)(g.gate + n);
+      if (any_in && m < g.M)
+        p.in[q] = *(const InT*)((const char*)src + ((int64_t)m * lds_in + n) * sizeof(p.in[q][0]));
+    }
+  };
+  auto widen = [](InT x) {
+    f32x4 f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = (float)x[r];
+    return f;
+  };
+  Piece cur, nxt;
+  load(0, cur);
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + 1 < 16) load(b + 1, nxt);
+    const int m = mb + 32 * (b >> 2);
+    if (m < g.M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = nb + 32 * (b & 3) + 8 * q;
+        if (n >= g.N) continue;
+        const f32x16& t = acc[b >> 2][b & 3];
+        const f32x4 v = {t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]};
+        if (EPI == EPI_F32) {   // in = 0 unless accumulating: one branch-free form (-0 -> +0)
+          *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = v + widen(cur.in[q]);
+        } else if (EPI == EPI_DGELU) {
+          const f32x4 pre = widen(cur.in[q]);
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
+          *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+        } else {
+          float y[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + cur.bias[q][r]);
+          if (EPI == EPI_BF16) {
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
+            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+          } else if (EPI == EPI_GELU) {
+            bf16x4 o, pre;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              pre[r] = f2bf(y[r]);
+              o[r] = f2bf(gelu_tanh(y[r]));
+            }
+            if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
+            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
+          } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
+            if (g.aux) {
+              bf16x4 yo;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
+              *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
+            }
+            const f32x4 res = widen(cur.in[q]);
+            f32x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], cur.gate[q][r]);
+            *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
+          }
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
+  int tm, tn;
+  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // ring / DMA exactly as gemm4w_kernel (see there): ns = K / 32 even and >= 4 (host check)
+  const int ns = g.K / BK4;
+  const i32x4 srd_a = A_KC ? make_srd(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(g.M - m0) * g.lda * 2))
+                           : make_srd(g.A + m0, (uint32_t)((int64_t)g.K * g.lda * 2 - (int64_t)m0 * 2));
+  const i32x4 srd_b = B_KC ? make_srd(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(g.N - n0) * g.ldb * 2))
+                           : make_srd(g.B + n0, (uint32_t)((int64_t)g.K * g.ldb * 2 - (int64_t)n0 * 2));
+  uint32_t offa[4], offb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    offa[i] = piece_off32<A_KC>(g.lda, wid, lane, i);
+    offb[i] = piece_off32<B_KC>(g.ldb, wid, lane, i);
+  }
+  auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
+  auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
+  auto issue = [&](int j) {
+    j = min(j, ns - 1);
+    char* st = smem + (j & 3) * SLICE4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_buf(srd_a, offa[i], soff_a(j), lds_addr(st + (wid * 4 + i) * 1024));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dma16_buf(srd_b, offb[i], soff_b(j), lds_addr(st + HALF4 + (wid * 4 + i) * 1024));
+  };
+  // fragment c = 4 s + i: k-step s, 32-row block i of the wave's 128 rows (A) / columns (B)
+  auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+    const char* st = smem + (j & 3) * SLICE4;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) af[c] = read_frag32<A_KC>(st, wm * 128 + (c & 3) * 32, c >> 2, lane);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bf[c] = read_frag32<B_KC>(st + HALF4, wn * 128 + (c & 3) * 32, c >> 2, lane);
+  };
+  auto step = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own part of slice j+1 landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int jd = min(j + 3, ns - 1);
+    char* sd = smem + ((j + 3) & 3) * SLICE4;
+    const char* st = smem + ((j + 1) & 3) * SLICE4;
+    // eight chunks: chunk c = (k-step s, A block i) runs its 4 MFMAs beside one LDS-DMA piece of
+    // slice j+3 and the reads of fragments c of slice j+1
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < 4) dma16_buf(srd_a, offa[c], soff_a(jd), lds_addr(sd + (wid * 4 + c) * 1024));
+      else dma16_buf(srd_b, offb[c - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + c - 4) * 1024));
+      na[c] = read_frag32<A_KC>(st, wm * 128 + (c & 3) * 32, c >> 2, lane);
+      nb[c] = read_frag32<B_KC>(st + HALF4, wn * 128 + (c & 3) * 32, c >> 2, lane);
+      const int s = c >> 2, i = c & 3;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)   // D = B . A^T: lanes own consecutive n of one row m
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+                     : "+a"(acc[i][jj]) : "v"(cb[4 * s + jj]), "v"(ca[c]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  asm volatile("s_nop 7" ::: "memory");    // accumulator zeroing (VALU) -> first asm MFMA
+  issue(0);
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 fa[8], fb[8], ga[8], gb[8];
+  read(0, fa, fb);
+  for (int j = 0; j < ns; j += 2) {
+    step(j, fa, fb, ga, gb);
+    step(j + 1, ga, gb, fa, fb);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // inline-asm MFMAs: pad the last MFMA write -> v_accvgpr_read distance by hand (32x32: 16 passes)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  const int mb = m0 + wm * 128 + (lane & 31), nb = n0 + wn * 128 + 4 * (lane >> 5);
+  if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
+    epilogue4x<EPI, true>(g, acc, mb, nb);
+  else
+    epilogue4x<EPI, false>(g, acc, mb, nb);
+}
+
 // tile: 0 = by shape (the 256 tile wherever it applies and fills >= 96 CUs), 128 / 256 = forced,
 // 512 = the 256 tile on the 8-wave kernel
 // (parity tests: both kernels accumulate every element in the same k order, so their outputs
@@ -763,6 +996,13 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
 #endif
 #ifndef GEMM_RESID_4W
 #define GEMM_RESID_4W 1
+#endif
+// the four-wave tile on MFMA 32x32x16 (gemm4x_kernel) for every epilogue (1), or only for the
+// weight gradients dW = dY^T X (0): there it is 1.3-6 % faster, on the forward / dX shapes 1-7 %
+// slower (720p x 81f, one process, 5 interleaved reps: profiles/r03_gemm_mfma32_ab.txt); the
+// outputs of the two kernels are bit-identical on every shape measured
+#ifndef GEMM_MFMA32
+#define GEMM_MFMA32 0
 #endif
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
@@ -781,7 +1021,9 @@ int launch(const GemmArgs& g, hipStream_t s, int tile) {
     const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
     const bool four = (GEMM_GELU_4W || EPI != EPI_GELU) && (GEMM_RESID_4W || EPI != EPI_RESID) &&
                       bytes_a < (1ll << 32) && bytes_b < (1ll << 32);
-    if (four)
+    if (four && (GEMM_MFMA32 || (EPI == EPI_F32 && !A_KC && !B_KC)))
+      hipLaunchKernelGGL((gemm4x_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
+    else if (four)
       hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
     else
       hipLaunchKernelGGL((gemm256s_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(NT2), 0, s, g);

@@ -99,6 +99,10 @@ def main():
                     if r:
                         ts[i].append(e0.elapsed_time(e1))
             same = all(torch.equal(outs[0][pas], o[pas]) for o in outs[1:]) if pas != "dwacc" else "n/a"
+            if same is False:      # different MFMA shapes round differently: report how far
+                r0 = outs[0][pas].float()
+                same = "rel " + ",".join(f"{((o[pas].float() - r0).norm() / r0.norm()).item():.1e}"
+                                         for o in outs[1:])
             meds = [statistics.median(t) for t in ts]
             print(f"{name:5s} {pas:3s}: " + " | ".join(f"lib{i} {m:6.2f} ms {fl / m / 1e9:5.0f} TF/s"
                                                        for i, m in enumerate(meds))
