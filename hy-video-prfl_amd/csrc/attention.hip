@@ -165,6 +165,10 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // ends Y_t, one phase before X_{t+1} reads it.
 // (720p forward 96.18 -> 95.29 ms in one-process A/B, outputs bit-identical:
 // profiles/r03_ab_attn_g0dma.txt)
+// 0: exact online max (rescale whenever a row max grows); > 0: lazy rescale (guide T13)
+#ifndef ATTN_LAZY_TAU
+#define ATTN_LAZY_TAU 0
+#endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
@@ -339,7 +343,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = xhalf_max(mx);
       const float mnew = fmaxf(m, mx * a.sl2);
-      if (__any(mnew > m)) {                    // rescale only when a row max grew
+      // rescale only when a row max grew (by more than ATTN_LAZY_TAU, log2 units: until then P
+      // is taken against the stale max, <= 2^TAU, and O, l and the LSE stay consistent)
+      if (__any(mnew > m + (float)ATTN_LAZY_TAU)) {
         const float alpha = __builtin_amdgcn_exp2f(m - mnew);
         lsum *= alpha;
 #pragma unroll
@@ -403,7 +409,14 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 
 // ============================================================================ backward ===
 // ============================================================================ backward ===
-// delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128)
+// delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128); stored negated under
+// ATTN_BWD_NEGD: the dK/dV kernel starts its dP = dO.V^T accumulators from -D (4 LDS reads of
+// the staged D rows straight into the accumulator registers), so the MFMA chain yields dP - D
+// directly: one VALU subtraction per score element less (dQ, whose 16 accumulator registers
+// would each need a move of its lane's one -D, adds it instead)
+#ifndef ATTN_BWD_NEGD
+#define ATTN_BWD_NEGD 0
+#endif
 __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
                                   const bf16* __restrict__ O, int64_t ldo, int64_t bo,
                                   float* __restrict__ delta, int B, int Lq, int H) {
@@ -423,7 +436,7 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int
   }
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
-  if (row < nrows && part == 0) delta[(b * H + h) * Lq + q] = acc;
+  if (row < nrows && part == 0) delta[(b * H + h) * Lq + q] = ATTN_BWD_NEGD ? -acc : acc;
 }
 
 // dK, dV with 8 waves (two per SIMD): 256 keys per workgroup, 32 per wave with the K^T
@@ -525,6 +538,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       f32x16 sacc, dpt;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpt[r] = 0.f; }
+      if (ATTN_BWD_NEGD) {    // dP accumulators start at -D of their query rows
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const f32x4 d4 = *(const f32x4*)(Ls + 64 + qt * 32 + 8 * rg + 4 * hh);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dpt[rg * 4 + r] = d4[r];
+        }
+      }
       const int row = qt * 32 + l32;
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -543,7 +564,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         for (int r = 0; r < 4; ++r) {
           const float p = __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]);
           sacc[rg * 4 + r] = p;
-          dpt[rg * 4 + r] = p * (dpt[rg * 4 + r] - d4[r]);
+          dpt[rg * 4 + r] = ATTN_BWD_NEGD ? p * dpt[rg * 4 + r] : p * (dpt[rg * 4 + r] - d4[r]);
         }
         if (__builtin_expect(tail, 0)) {   // rows past Lq: P = dS = 0 (last tile only)
 #pragma unroll
@@ -701,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
-        dpt[r] = p * (dpt[r] - del);
+        dpt[r] = ATTN_BWD_NEGD ? p * (dpt[r] + del) : p * (dpt[r] - del);   // del = -D there
       }
       if (__builtin_expect(kb + kt * 32 + 32 > a.k_len, 0)) {   // keys >= k_len: dS = 0
 #pragma unroll

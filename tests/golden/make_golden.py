@@ -372,7 +372,18 @@ TRAINER_SFT_IDX = (613, 287)
 TRAINER_MID = (2, 1)
 
 
-def _trainer_run(truth):
+def _bump_ulps(t, name, n=8):
+    """t (bf16-valued) with n seeded elements moved by one bf16 ulp: a perturbation at the
+    resolution of the bf16 state, to sample the chain's own bf16 noise floor."""
+    flat = t.to(torch.bfloat16).flatten().clone()
+    idx = torch.from_numpy((np.abs(seeded.randn(name, (n,))) * 1e6).astype(np.int64) % flat.numel())
+    bits = flat.view(torch.int16)
+    sign = torch.from_numpy(np.sign(seeded.randn(name + ".s", (n,)))).to(torch.int16)
+    bits[idx] += sign
+    return bits.view(torch.bfloat16).view(t.shape).to(t.dtype)
+
+
+def _trainer_run(truth, perturb=None):
     """Two PRFL iterations (step 0, then step 1 = an optimizer-step boundary for
     gradient_accumulation_steps 2) restating `train_prfl.py` on the reference modules:
     `train_step` (`:900-980`: flow-matching SFT loss / GA, backward, `clip_grad_norm_(1.0)`,
@@ -453,6 +464,8 @@ def _trainer_run(truth):
             ts = sch.timesteps
             latent = torch.from_numpy(seeded.randn(f"trainer.rwd_noise.{step}", (1,) + TOY_LATENT)) \
                 .to(torch.bfloat16).to(lat_dt)
+            if perturb is not None:
+                latent = _bump_ulps(latent, f"trainer.perturb.{perturb}.{step}")
             mid = TRAINER_MID[step]
             with torch.no_grad():
                 for i in range(mid):
@@ -480,13 +493,44 @@ def _trainer_run(truth):
         M.flash_attention = saved
 
 
+def _fresh_err_stats(run, t32, tag):
+    """(median, max) over parameters of the rel-L2 of a run's fresh gradient vs the truth's."""
+    errs = []
+    for k, v in run.items():
+        if k.startswith(tag + ":fresh:") and ("/full/" in k.replace(":fresh:", "/") or
+                                              "/head/" in k.replace(":fresh:", "/")):
+            t = t32[k]
+            errs.append(float(np.linalg.norm(v - t) / max(np.linalg.norm(t), 1e-30)))
+    errs.sort()
+    return errs[len(errs) // 2], errs[-1]
+
+
+TRAINER_PERTURB = 8
+
+
 def case_toy_prfl_trainer():
-    """PRFLTrainer parity: the reference run and its fp32 truth."""
+    """PRFLTrainer parity: the reference run, its fp32 truth, and the reference's
+    own bf16 noise floor through the reward chain: TRAINER_PERTURB more reference runs whose
+    reward-step initial noise differs by one bf16 ulp in 8 elements (the chain amplifies state
+    perturbations at bf16 resolution ~10x, so one bf16 run's distance to the truth is a draw from
+    this spread, not a fixed number)."""
     ref = _trainer_run(truth=False)
     t32 = _trainer_run(truth=True)
+    tags = [f"it{s}:{p}" for s in (0, 1) for p in ("sft", "rwd")]
+    floor = {t: [] for t in tags}
+    for i in range(TRAINER_PERTURB):
+        run = _trainer_run(truth=False, perturb=i)
+        for t in tags:
+            floor[t].append(_fresh_err_stats(run, t32, t))
+    extra = {}
+    for t in tags:
+        extra[f"floor:{t}:med"] = np.asarray([m for m, _ in floor[t]])
+        extra[f"floor:{t}:max"] = np.asarray([x for _, x in floor[t]])
+        print(t, "reference runs' median err vs truth:", np.round(extra[f"floor:{t}:med"], 4),
+              "max:", np.round(extra[f"floor:{t}:max"], 4))
     save("toy_prfl_trainer", ga=np.float64(TRAINER_GA), lr=np.float64(TRAINER_LR),
          sft_idx=np.asarray(TRAINER_SFT_IDX), mid=np.asarray(TRAINER_MID), **ref,
-         **{"t32:" + k: v for k, v in t32.items()})
+         **{"t32:" + k: v for k, v in t32.items()}, **extra)
 
 
 def _exact_attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=None,

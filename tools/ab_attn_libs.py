@@ -72,6 +72,19 @@ def main():
         same = all(torch.equal(outs[0][n], o[n]) for o in outs[1:] for n in keys)
         print(f"{w}: " + " | ".join(f"lib{i} {m:.2f} ms {fl / m / 1e9:.0f} TF/s" for i, m in enumerate(meds))
               + f" | identical {same}", flush=True)
+        if w == "fwd" and not same:
+            # accuracy of every build vs an exact fp64 softmax attention on sampled rows / heads
+            rows = torch.linspace(0, L - 1, 48, device=dev).long()
+            errs = [[] for _ in libs]
+            for h in (0, 17, 39):
+                sl = slice(h * 128, (h + 1) * 128)
+                qq, kk, vv = q[rows, sl].double(), k[:, sl].double(), v[:, sl].double()
+                ref = torch.softmax(qq @ kk.T * sc, -1) @ vv
+                for i in range(len(libs)):
+                    o = outs[i]["o"][rows, sl].double()
+                    errs[i].append(((o - ref).norm() / ref.norm()).item())
+            print("fwd rel-L2 vs fp64 (48 rows x 3 heads): " +
+                  " | ".join(f"lib{i} {max(e):.2e}" for i, e in enumerate(errs)), flush=True)
 
 
 if __name__ == "__main__":
