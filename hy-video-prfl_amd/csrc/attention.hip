@@ -165,9 +165,14 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // ends Y_t, one phase before X_{t+1} reads it.
 // (720p forward 96.18 -> 95.29 ms in one-process A/B, outputs bit-identical:
 // profiles/r03_ab_attn_g0dma.txt)
-// 0: exact online max (rescale whenever a row max grows); > 0: lazy rescale (guide T13)
+// 0: exact online max (rescale whenever a row max grows); > 0: lazy rescale (guide T13): the
+// O / l rescale runs only when some row max grew by more than TAU (log2 units), so P is taken
+// against a max up to TAU stale (P <= 2^TAU: fp32 O and l have the headroom, and bf16 P rounds
+// with the same relative error at any scale).  TAU = 8: 720p forward 100.22 -> 95.98 ms (+4.4 %),
+// rel-L2 vs an fp64 softmax attention 2.33e-3 -> 2.38e-3 on sampled rows
+// (profiles/r03_ab_attn_lazy.txt)
 #ifndef ATTN_LAZY_TAU
-#define ATTN_LAZY_TAU 0
+#define ATTN_LAZY_TAU 8
 #endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
@@ -414,8 +419,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 // the staged D rows straight into the accumulator registers), so the MFMA chain yields dP - D
 // directly: one VALU subtraction per score element less (dQ, whose 16 accumulator registers
 // would each need a move of its lane's one -D, adds it instead)
+// (720p backward 340.0 -> 332.7 ms, profiles/r03_ab_attn_negd.txt)
 #ifndef ATTN_BWD_NEGD
-#define ATTN_BWD_NEGD 0
+#define ATTN_BWD_NEGD 1
 #endif
 __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
                                   const bf16* __restrict__ O, int64_t ldo, int64_t bo,

@@ -429,11 +429,15 @@ def test_toy_pavrm_steps_vs_reference(golden):
             for p, gr in zip(ps, grads[tag]):
                 p.grad = gr
             ref.step()
+            moved = 0.0
             for p, q, p0 in zip(ps, opt.params, orig_step[tag]):
                 # updates compared, not parameters: one AdamW step moves an element by ~lr, so
                 # a bound tied to |p| could not see a skipped update
                 d_ref, d_ours = p.detach() - p0, q.detach() - p0
                 tol = 1e-3 * 1e-6 + 4 * torch.finfo(torch.float32).eps * p0.abs()
                 assert bool(((d_ours - d_ref).abs() <= tol).all())
-                assert d_ref.abs().max().item() > 0.5e-6        # the step did move the tensor
+                moved = max(moved, d_ref.abs().max().item())
+            # the step did move the parameters by ~lr (tensors whose gradients are far below
+            # AdamW's eps move by much less: lr * |g| / (|g| + eps))
+            assert moved > 0.5e-6, (tag, moved)
             ref_states[tag] = ref.state_dict()
