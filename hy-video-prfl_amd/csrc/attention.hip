@@ -419,6 +419,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 // the staged D rows straight into the accumulator registers), so the MFMA chain yields dP - D
 // directly: one VALU subtraction per score element less (dQ, whose 16 accumulator registers
 // would each need a move of its lane's one -D, adds it instead)
+#ifndef ATTN_BWD_DMA_MID
+#define ATTN_BWD_DMA_MID 0
+#endif
 // (720p backward 340.0 -> 332.7 ms, profiles/r03_ab_attn_negd.txt)
 #ifndef ATTN_BWD_NEGD
 #define ATTN_BWD_NEGD 1
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   __syncthreads();
   for (int t = 0; t < nq; ++t) {
     const int st = t & 1;
-    if (t + 1 < nq) dma_tile(t + 1, st ^ 1);
+    if (!ATTN_BWD_DMA_MID && t + 1 < nq) dma_tile(t + 1, st ^ 1);
     const char* Qs = smem + V_BYTES + st * STAGE;
     const char* Ds = Qs + 16384;
     const float* Ls = (const float*)(Qs + 32768);
@@ -578,6 +581,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
             if (qb + q4 + r >= a.Lq) { sacc[rg * 4 + r] = 0.f; dpt[rg * 4 + r] = 0.f; }
         }
       }
+      if (ATTN_BWD_DMA_MID && qt == 0 && t + 1 < nq) dma_tile(t + 1, st ^ 1);
       bf16x8 pk[2], dk8[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -709,8 +713,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   __syncthreads();
   for (int t = 0; t < nkv; ++t) {
     const int kb = (t0 + t) * TK;
-    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it)
-    if (t + 1 < nkv) dma(t + 1, (t + 1) & 1);
+    // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it);
+    // ATTN_BWD_DMA_MID: issued after the first key sub-tile's VALU block instead (LDS-DMA issue
+    // costs less there than beside MFMAs and LDS reads)
+    if (!ATTN_BWD_DMA_MID && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
     const char* Ks = smem + (t & 1) * SB;
     const char* Vs = Ks + SV;
     bf16x8 dsp[NKT][2];
@@ -740,6 +746,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
                                f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
                                f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+      if (ATTN_BWD_DMA_MID && kt == 0 && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
     }
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {

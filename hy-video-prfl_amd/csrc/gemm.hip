@@ -651,9 +651,6 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
   }
 }
 
-#ifndef GEMM_DIAG
-#define GEMM_DIAG 0
-#endif
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
@@ -717,9 +714,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      // GEMM_DIAG (timing diagnostics only, wrong results): 1 = no in-loop DMA, 2 = A only
-      if (GEMM_DIAG == 1 || (GEMM_DIAG == 2 && i >= 4)) {
-      } else if (i < 4) dma16_buf(srd_a, offa[i], soff_a(jd), lds_addr(sd + (wid * 4 + i) * 1024));
+      if (i < 4) dma16_buf(srd_a, offa[i], soff_a(jd), lds_addr(sd + (wid * 4 + i) * 1024));
       else dma16_buf(srd_b, offb[i - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + i - 4) * 1024));
       na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
       nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
@@ -747,116 +742,6 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // the MFMAs are inline asm: the compiler does not see their AGPR writes, so pad the
   // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  const int mb = m0 + wm * 128 + (lane & 15), nb = n0 + wn * 128 + 4 * (lane >> 4);
-  if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
-    epilogue4w<EPI, true>(g, acc, mb, nb);
-  else
-    epilogue4w<EPI, false>(g, acc, mb, nb);
-}
-
-// ------------------------------- 256x256, four waves, register-staged operands (gemm4r) -----
-// gemm4w_kernel with the operands staged through VGPRs instead of LDS-DMA: per 32-deep slice each
-// wave issues 8 buffer_load_dwordx4 (its 8 KiB) into registers one step ahead and writes the
-// previous step's 8 as ds_write_b128 (lane-linear, the swizzle lives in the global source
-// offsets exactly as for the DMA).  Measured motivation (profiles/r03_gemm_dma_diag.txt): the
-// same loop without its in-loop LDS-DMA runs 1559-1631 TF/s vs 1245-1264 with it — the DMA
-// pieces' issue cost, not bandwidth, holds the four-wave loop at ~0.65 MFMA busy.
-// Ring: slot (j & 3) holds slice j; step j (MFMAs of slice j, fragment reads of slice j+1)
-// writes slice j+2 (loaded in step j-1) into slot (j+2) & 3 — last read in step j-3 — and loads
-// slice j+3; the lgkmcnt(0) + barrier opening step j+1 publishes slice j+2 before its reads.
-template <bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm4r_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
-  int tm, tn;
-  tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int ns = g.K / BK4;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(A_KC ? g.A + (int64_t)m0 * g.lda : g.A + m0), (short)0,
-      (int)(A_KC ? (int64_t)(g.M - m0) * g.lda * 2 : (int64_t)g.K * g.lda * 2 - (int64_t)m0 * 2),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(B_KC ? g.B + (int64_t)n0 * g.ldb : g.B + n0), (short)0,
-      (int)(B_KC ? (int64_t)(g.N - n0) * g.ldb * 2 : (int64_t)g.K * g.ldb * 2 - (int64_t)n0 * 2),
-      0x00020000);
-  uint32_t offa[4], offb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i);
-    offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i);
-  }
-  auto soff_a = [&](int j) { return (int)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
-  auto soff_b = [&](int j) { return (int)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
-  auto load_piece = [&](int j, int c) -> u32x4 {
-    return c < 4 ? __builtin_amdgcn_raw_buffer_load_b128(ra, offa[c], soff_a(j), 0)
-                 : __builtin_amdgcn_raw_buffer_load_b128(rb, offb[c - 4], soff_b(j), 0);
-  };
-  auto piece_lds = [&](int j, int c) {
-    return smem + (j & 3) * SLICE4 + (c < 4 ? 0 : HALF4) + (wid * 4 + (c & 3)) * 1024 + lane * 16;
-  };
-  auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
-    const char* st = smem + (j & 3) * SLICE4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) bf[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
-  };
-  auto step = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8],
-                  u32x4 (&wr)[8], u32x4 (&ld)[8]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own writes of slice j+1 landed
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // branch-free: past the last slice the loads re-fetch slice ns-1 and the writes land in a
-    // slot nobody reads again (its last reader ran in step j-3)
-    const int jl = min(j + 3, ns - 1);
-    const char* st = smem + ((j + 1) & 3) * SLICE4;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      ld[c] = load_piece(jl, c);
-      *(u32x4*)piece_lds(j + 2, c) = wr[c];
-      na[c] = read_frag4<A_KC>(st, wm * 128 + c * 16, lane);
-      nb[c] = read_frag4<B_KC>(st + HALF4, wn * 128 + c * 16, lane);
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                     : "+a"(acc[c][jj]) : "v"(cb[jj]), "v"(ca[c]));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  asm volatile("s_nop 7" ::: "memory");    // accumulator zeroing (VALU) -> first asm MFMA
-  u32x4 r0[8], r1[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) r0[c] = load_piece(0, c);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) r1[c] = load_piece(1, c);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) *(u32x4*)piece_lds(0, c) = r0[c];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) *(u32x4*)piece_lds(1, c) = r1[c];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) r1[c] = load_piece(2, c);      // written in step 0
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  bf16x8 fa[8], fb[8], ga[8], gb[8];
-  read(0, fa, fb);
-  for (int j = 0; j < ns; j += 2) {
-    step(j, fa, fb, ga, gb, r1, r0);
-    step(j + 1, ga, gb, fa, fb, r0, r1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   const int mb = m0 + wm * 128 + (lane & 15), nb = n0 + wn * 128 + 4 * (lane >> 4);
   if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
@@ -1119,9 +1004,6 @@ __global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
 #ifndef GEMM_MFMA32
 #define GEMM_MFMA32 0
 #endif
-#ifndef GEMM_REGSTAGE
-#define GEMM_REGSTAGE 0       // 1: register-staged operands (gemm4r_kernel) for every epilogue
-#endif
 template <bool A_KC, bool B_KC, int EPI>
 int launch(const GemmArgs& g, hipStream_t s, int tile) {
   const int nt256 = ((g.M + BM2 - 1) / BM2) * ((g.N + BN2 - 1) / BN2);
@@ -1139,9 +1021,7 @@ int launch(const GemmArgs& g, hipStream_t s, int tile) {
     const int64_t bytes_b = (B_KC ? (int64_t)g.N : (int64_t)g.K) * g.ldb * 2;
     const bool four = (GEMM_GELU_4W || EPI != EPI_GELU) && (GEMM_RESID_4W || EPI != EPI_RESID) &&
                       bytes_a < (1ll << 32) && bytes_b < (1ll << 32);
-    if (four && GEMM_REGSTAGE)
-      hipLaunchKernelGGL((gemm4r_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
-    else if (four && (GEMM_MFMA32 || (EPI == EPI_F32 && !A_KC && !B_KC)))
+    if (four && (GEMM_MFMA32 || (EPI == EPI_F32 && !A_KC && !B_KC)))
       hipLaunchKernelGGL((gemm4x_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
     else if (four)
       hipLaunchKernelGGL((gemm4w_kernel<A_KC, B_KC, EPI>), dim3(nt256), dim3(256), 0, s, g);
