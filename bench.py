@@ -50,6 +50,7 @@ import torch.distributed as dist  # noqa: E402
 
 C, F, NH, NL, TXT = 5120, 13824, 40, 40, 512
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0       # dense block-scaled e4m3 MFMA (2x bf16 per clock)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -249,7 +250,10 @@ def main():
     ap.add_argument("--mid", type=int, default=19, help="mid_timestep (E[randint(0,38)] = 19)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp8", action="store_true",
-                    help="config C5's fp8 path: e4m3 forward projections on the block-scaled MFMA")
+                    help="config C5's fp8 path: e4m3 forward projections and the e4m3 self-attention "
+                         "forward on the block-scaled MFMA")
+    ap.add_argument("--fp8-gemm-only", action="store_true",
+                    help="with --fp8: keep the self-attention forward bf16 (the round-2 fp8 path)")
     ap.add_argument("--budget-s", type=float, default=540.0,
                     help="wall-clock budget from interpreter start (warm-up + timed + CPU baseline)")
     ap.add_argument("--warmup-mid", type=int, default=1,
@@ -291,8 +295,8 @@ def main():
         i2v = "_i2v_" in args.workload
         gen, lrm, qa, mlp = build_models(dev, 110221, "i2v" if i2v else "t2v", toy=args.toy)
         if args.fp8:
-            gen.set_fp8_gemm(True)
-            lrm.set_fp8_gemm(True)
+            gen.set_fp8_gemm(True, attn=not args.fp8_gemm_only)
+            lrm.set_fp8_gemm(True, attn=not args.fp8_gemm_only)
         # keep the self-attention outputs of graph-recording block forwards for the backward
         # (bit-identical to recomputing them; block.py): the budget bounds the bytes kept at any
         # time.  T2V: 38 GB keeps all 40 generator blocks + the 8 reward-model blocks at 720p
@@ -425,10 +429,11 @@ def main():
     # roofline kernel: the dominant single kernel (one symbol, one shape) in the timed region —
     # the L x L self-attention forward (`attn_fwd_kernel<false>`); the GEMM family is reported
     # per family in "kernels" (it spans ten template instantiations and many shapes)
-    dom = "attn_fwd"
+    dom = "attn_fwd_fp8" if args.fp8 and not args.fp8_gemm_only and not c1 else "attn_fwd"
+    peak = PEAK_FP8_TFLOPS if dom == "attn_fwd_fp8" else PEAK_BF16_TFLOPS
     d = prof[dom]
     achieved = d["work"] / (d["ms"] * 1e-3) / 1e12 if d["count"] else 0.0
-    traffic, traffic_src = pmc_traffic(L)
+    traffic, traffic_src = pmc_traffic(L) if dom == "attn_fwd" else (None, None)
     value = world * steps / dt
     if c1:
         metric, unit = "C1 pre_480: 14B block forwards/s, 480p x 49f", "block forwards/s"
@@ -453,7 +458,8 @@ def main():
         "budget_s": args.budget_s, "wall_s_at_report": None,
         "ms_per_step": round(dt / steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp8-e4m3 fwd GEMMs / bf16" if args.fp8 else "bf16",
+        "dtype": ("fp8-e4m3 fwd GEMMs / bf16" if args.fp8_gemm_only else
+                  "fp8-e4m3 fwd GEMMs + self-attention fwd / bf16") if args.fp8 else "bf16",
         "data": "synthetic latents/text, random-init 14B weights",
         "config": {"workload": workload, "model": model, "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
@@ -467,9 +473,9 @@ def main():
                                     "workgroup 0 of every self-attention forward launch in the "
                                     "timed window; mean weighted by launch time"},
         "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 1),
-                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "peak_at_measured_clock": round(PEAK_BF16_TFLOPS * clock["mean_mhz"] / 2400.0, 1)
+                     "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4),
+                     "peak_at_measured_clock": round(peak * clock["mean_mhz"] / 2400.0, 1)
                      if clock["mean_mhz"] else None,
                      "launches": d["count"],
                      "avg_launch_ms": round(d["ms"] / d["count"], 3) if d["count"] else None,

@@ -413,14 +413,16 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward ===
-// ============================================================================ backward ===
 // delta[b][h][q] = sum_d dO * O  (16 lanes per (q, h) row of 128); stored negated under
 // ATTN_BWD_NEGD: the dK/dV kernel starts its dP = dO.V^T accumulators from -D (4 LDS reads of
 // the staged D rows straight into the accumulator registers), so the MFMA chain yields dP - D
 // directly: one VALU subtraction per score element less (dQ, whose 16 accumulator registers
 // would each need a move of its lane's one -D, adds it instead)
+// ATTN_BWD_DMA_MID: the dK/dV and dQ kernels issue their next-tile LDS-DMA after the first
+// sub-tile's VALU block instead of at the top of the step, out of the MFMA-dense opening
+// (720p backward 318.8 -> 316.8 ms, outputs bit-identical: profiles/r03_ab_attn_bwd_dmamid.txt)
 #ifndef ATTN_BWD_DMA_MID
-#define ATTN_BWD_DMA_MID 0
+#define ATTN_BWD_DMA_MID 1
 #endif
 // (720p backward 340.0 -> 332.7 ms, profiles/r03_ab_attn_negd.txt)
 #ifndef ATTN_BWD_NEGD
@@ -866,6 +868,437 @@ __global__ __launch_bounds__(256) void attn_merge_q_kernel(AttnBwdArgs a) {
   }
 }
 
+// ====================================================== low-precision forward (config C5) ====
+// Self-attention forward at twice the bf16 MFMA rate (SageAttention-style split of precisions):
+//   S = Q.K^T on the int8 MFMA v_mfma_i32_32x32x32_i8: Q int8 per (token, head), scale
+//     sq = amax / 127; K int8 per (128-key tile, head), sk[tile] = amax / 127.  A uniform 8-bit
+//     grid over each row / tile keeps the score error ~5x below e4m3's 3-bit mantissa (the
+//     Q.K^T error is what the softmax exponentiates).  Exact i32 accumulation.
+//   O = P.V on the block-scaled e4m3 MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (E8M0 scales 2^0):
+//     V e4m3 per (head, channel d), sv[d] = amax / 448, stored TRANSPOSED (V^T [d][key]) so the
+//     product reads plain rows (there is no transposed 8-bit LDS read to lean on); P e4m3
+//     against the running max shifted by OFF = log2(440) - TAU (P <= 440 < 448 for a max up to
+//     TAU stale; values down to 2^-9 / 440 of the row max survive as e4m3 subnormals).
+// Folded dequantisation: S^T[key][q] has q on the lane, so exp2(S sl2 - m) = exp2(acc c - mb)
+// with c = sq[q] sk[tile] sl2 (one multiply per tile); O^T[d][q] has d on the accumulator row,
+// so sv[d] is applied once, in the epilogue.  Row sums come out of the PV MFMA: a fifth O^T
+// tile whose A operand is a register constant (row 0 all ones) sums the QUANTISED P, so the
+// normaliser matches the numerator's weights exactly and the 64 v_add per tile are gone.
+// k-slot maps: Q.K^T sums over d in natural order on both operands (half hh of step s = d
+// 32s + 16hh + j); P^T from the S^T accumulators of 32-key sub-tiles 2ks, 2ks+1 is byte j =
+// register j of sub-tile 2ks (j < 16) / 2ks+1 (j >= 16), i.e. key 32(j>>4) + (j&3) +
+// 8((j>>2)&3) + 4hh of the 64-key step, and V^T stores that key at byte 32hh + j of the step
+// (fp8_vt_pos), so a lane reads its 32 V^T bytes as two plain 16-B chunks.
+// Tiles of TK = 128 keys (a 16-KiB K image [key][128 B] and a 16-KiB V^T image [d][128 B],
+// 16-B chunks XOR-swizzled by (row >> 1) & 7: the 16 lanes of one ds_read_b128 pass hit 16
+// different bank groups), 3-stage ring (96 KiB); otherwise the bf16 kernel's schedule: 8 waves x
+// 32 queries, two barrier-delimited phases per tile (X: 16 QK + 10 PV MFMAs; Y: softmax), waves
+// 4-7 one barrier behind at priority 1, XCD grouping, split-KV tail through attn_merge_kernel.
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(16))) int i32x16;
+
+__device__ __forceinline__ f32x16 mfma8(i32x8 a, i32x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0,
+                                                         0x7f7f7f7f);
+}
+__device__ __forceinline__ i32x16 mfmai8(i32x4 a, i32x4 b, i32x16 c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int fp8_vt_pos(int key64) {   // byte of key key64 in its V^T step
+  const int kk = key64 & 31;
+  return 32 * ((kk >> 2) & 1) + 16 * (key64 >> 5) + (kk & 3) + 4 * (kk >> 3);
+}
+__device__ __forceinline__ int f8swz(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+constexpr float FP8_QMAX = 448.f, I8_QMAX = 127.f;
+
+struct AttnF8Args {
+  AttnArgs base;                 // O / LSE / shapes / split tail (Q, K, V: the bf16 inputs)
+  const int8_t* Q8;              // [B][Lq][H*128] int8
+  const float* sq;               // [B][H][Lq]
+  const int8_t* K8;              // [B][Lk][H*128] int8
+  const float* sk;               // [B][H][lkp / 128]
+  const uint8_t* Vt8;            // [B][H][128][lkp] e4m3, keys permuted per 64 (fp8_vt_pos)
+  const unsigned* vamax;         // [B][H][128] fp32 bits of amax |V[:, d]|
+  int64_t lkp;                   // padded key count (multiple of 128; pad bytes are zeros)
+};
+
+// amax |V[:, d]| per (sample, head, d) over 256-key blocks: grid (ceil(Lk / 256), H, B), 256
+// threads = 16 key rows x 16 chunks of 8 d.  Non-negative fp32 bits order as unsigned integers:
+// unsigned atomicMax (vector-memory atomics) into a zeroed buffer.
+__global__ __launch_bounds__(256) void attn_lp_vamax_kernel(AttnF8Args f) {
+  const AttnArgs& a = f.base;
+  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 256;
+  const int ch = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  float vm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = k0 + rg; r < min(k0 + 256, a.Lk); r += 16) {
+    const bf16x8 vv = *(const bf16x8*)(a.V + b * a.bv + (int64_t)r * a.ldv + h * HD + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vm[j] = fmaxf(vm[j], fabsf(bf2f(vv[j])));
+  }
+  __shared__ float red[4][128];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    vm[j] = fmaxf(vm[j], __shfl_xor(vm[j], 16, 64));
+    vm[j] = fmaxf(vm[j], __shfl_xor(vm[j], 32, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][ch * 8 + j] = vm[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const float v = fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]),
+                          fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
+    atomicMax((unsigned*)f.vamax + ((int64_t)b * a.H + h) * HD + threadIdx.x, __float_as_uint(v));
+  }
+}
+
+__device__ __forceinline__ unsigned pack_i8(float x0, float x1, float x2, float x3) {
+  return ((unsigned)__float2int_rn(x0) & 0xffu) | (((unsigned)__float2int_rn(x1) & 0xffu) << 8) |
+         (((unsigned)__float2int_rn(x2) & 0xffu) << 16) | ((unsigned)__float2int_rn(x3) << 24);
+}
+__device__ __forceinline__ unsigned cvt4_fp8(float x0, float x1, float x2, float x3) {
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(x0, x1, 0, false);
+  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(x2, x3, r, true);
+}
+// 64 bf16 -> 64 int8 (x * inv, round to nearest even) as 4 x 16 B
+__device__ __forceinline__ void quant64_i8(const bf16* src, float inv, int8_t* dst) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const bf16x8 v0 = *(const bf16x8*)(src + c * 16), v1 = *(const bf16x8*)(src + c * 16 + 8);
+    u32x4 o;
+    o[0] = pack_i8(bf2f(v0[0]) * inv, bf2f(v0[1]) * inv, bf2f(v0[2]) * inv, bf2f(v0[3]) * inv);
+    o[1] = pack_i8(bf2f(v0[4]) * inv, bf2f(v0[5]) * inv, bf2f(v0[6]) * inv, bf2f(v0[7]) * inv);
+    o[2] = pack_i8(bf2f(v1[0]) * inv, bf2f(v1[1]) * inv, bf2f(v1[2]) * inv, bf2f(v1[3]) * inv);
+    o[3] = pack_i8(bf2f(v1[4]) * inv, bf2f(v1[5]) * inv, bf2f(v1[6]) * inv, bf2f(v1[7]) * inv);
+    *(u32x4*)(dst + c * 16) = o;
+  }
+}
+__device__ __forceinline__ float amax64(const bf16* src) {
+  float am = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 v = *(const bf16x8*)(src + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf2f(v[j])));
+  }
+  return am;
+}
+
+// Quantisation of one 128-row block (= one key tile) of one (sample, head): grid
+// (ceil(max(Lq, lkp) / 128), H, B), 256 threads = 128 rows x 2 halves of 64 d.  Q rows -> Q8 +
+// sq, K rows -> K8 + the tile's sk, V rows -> the tile's [128 d][128 key] V^T image in LDS
+// (keys permuted per 64, rows >= Lk zero) -> Vt8.
+__global__ __launch_bounds__(256) void attn_lp_quant_kernel(AttnF8Args f) {
+  const AttnArgs& a = f.base;
+  const int b = blockIdx.z, h = blockIdx.y, r0 = blockIdx.x * 128;
+  const int hf = threadIdx.x & 1, row = r0 + (threadIdx.x >> 1);
+  const int64_t ld8 = (int64_t)a.H * HD;
+  if (row < a.Lq) {
+    const bf16* src = a.Q + b * a.bq + (int64_t)row * a.ldq + h * HD + hf * 64;
+    float am = amax64(src);
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    quant64_i8(src, am > 0.f ? I8_QMAX / am : 0.f,
+               (int8_t*)f.Q8 + ((int64_t)b * a.Lq + row) * ld8 + h * HD + hf * 64);
+    if (hf == 0) ((float*)f.sq)[((int64_t)b * a.H + h) * a.Lq + row] = am > 0.f ? am / I8_QMAX : 1.f;
+  }
+  if (r0 >= f.lkp) return;
+  __shared__ float kred[4];
+  {
+    const bf16* src = a.K + b * a.bk + (int64_t)min(row, a.Lk - 1) * a.ldk + h * HD + hf * 64;
+    float am = row < a.Lk ? amax64(src) : 0.f;
+    am = wave_max(am);
+    if ((threadIdx.x & 63) == 0) kred[threadIdx.x >> 6] = am;
+    __syncthreads();
+    am = fmaxf(fmaxf(kred[0], kred[1]), fmaxf(kred[2], kred[3]));
+    if (row < a.Lk)
+      quant64_i8(src, am > 0.f ? I8_QMAX / am : 0.f,
+                 (int8_t*)f.K8 + ((int64_t)b * a.Lk + row) * ld8 + h * HD + hf * 64);
+    if (threadIdx.x == 0)
+      ((float*)f.sk)[((int64_t)b * a.H + h) * (f.lkp >> 7) + blockIdx.x] = am > 0.f ? am / I8_QMAX : 1.f;
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t vt[HD][128];
+  {
+    const unsigned* vam = f.vamax + ((int64_t)b * a.H + h) * HD + hf * 64;
+    const int key = row - r0, pos = 64 * (key >> 6) + fp8_vt_pos(key & 63);
+    const bool live = row < a.Lk;
+    const bf16* src = a.V + b * a.bv + (int64_t)min(row, a.Lk - 1) * a.ldv + h * HD + hf * 64;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16x8 v = *(const bf16x8*)(src + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float a0 = __uint_as_float(vam[c * 8 + j]), a1 = __uint_as_float(vam[c * 8 + j + 1]);
+        const float x0 = live && a0 > 0.f ? bf2f(v[j]) * (FP8_QMAX / a0) : 0.f;
+        const float x1 = live && a1 > 0.f ? bf2f(v[j + 1]) * (FP8_QMAX / a1) : 0.f;
+        const unsigned pk = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(x0, x1, 0, false);
+        vt[hf * 64 + c * 8 + j][pos] = (uint8_t)(pk & 0xff);
+        vt[hf * 64 + c * 8 + j + 1][pos] = (uint8_t)((pk >> 8) & 0xff);
+      }
+    }
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x >> 1;
+    uint8_t* dst = (uint8_t*)f.Vt8 + (((int64_t)b * a.H + h) * HD + d) * f.lkp + r0 + hf * 64;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(u32x4*)(dst + 16 * c) = *(const u32x4*)&vt[d][hf * 64 + 16 * c];
+  }
+}
+
+#ifndef ATTN_LP_TAU
+#define ATTN_LP_TAU 2
+#endif
+#ifndef ATTN_LP_SUM_MFMA
+#define ATTN_LP_SUM_MFMA 1
+#endif
+#ifndef ATTN_LP_SCHED
+#define ATTN_LP_SCHED 1
+#endif
+template <int SCHED>
+__global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
+  const AttnArgs& a = f.base;
+  constexpr int TK = 128, SV = 16384, SB = 2 * SV;
+  constexpr float TAU = (float)ATTN_LP_TAU;
+  const float OFF = 8.78135971f - TAU;          // log2(440) - TAU
+  // ring of [K | V^T] tiles, then each wave's 32 int8 Q rows (read per tile: the Q fragments
+  // would hold 16 VGPRs through the softmax phase)
+  __shared__ __attribute__((aligned(16))) char smem[3 * SB + 8 * 4096];
+  const int bid = blockIdx.x;
+  const bool part = bid >= a.nmain;
+  const int unit = part ? a.nmain + (bid - a.nmain) / a.split : bid;
+  const bool clk = a.clk != nullptr && bid == 0 && threadIdx.x == 0;
+  unsigned long long c0 = 0, w0 = 0;
+  if (clk) {
+    c0 = clock64();
+    w0 = wall_clock64();
+  }
+  int bh, tile;
+  xcd_tile((a.Lq + 255) >> 8, a.B * a.H, bh, tile, unit);
+  const int b = bh / a.H, h = bh % a.H, q0 = tile * 256;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gp = w >> 2;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int64_t ld8 = (int64_t)a.H * HD;
+  char* Qs = smem + 3 * SB + w * 4096;
+  const int8_t* Kb = f.K8 + (int64_t)b * a.Lk * ld8 + h * HD;
+  const uint8_t* Vb = f.Vt8 + ((int64_t)b * a.H + h) * HD * f.lkp;
+  const float* skb = f.sk + ((int64_t)b * a.H + h) * (f.lkp >> 7);
+
+  float cq;
+  {
+    const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
+    const int8_t* src = f.Q8 + ((int64_t)b * a.Lq + qr) * ld8 + h * HD + 16 * hh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *(i32x4*)(Qs + f8swz(l32, 2 * s + hh)) = *(const i32x4*)(src + 32 * s);
+    cq = f.sq[((int64_t)b * a.H + h) * a.Lq + qr] * a.sl2;
+  }
+  // A operand of the row-sum MFMA: a 32 x 64 block of e4m3 1.0 (0x38): every row of the fifth
+  // O^T tile is the row sum
+  constexpr int one = 0x38383838;
+  const i32x8 ones = {one, one, one, one, one, one, one, one};
+  constexpr int NO = ATTN_LP_SUM_MFMA ? 5 : 4;
+  f32x16 o[NO];
+  float lsum = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < NO; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = NEG_INF, mb = NEG_INF;
+  int t0 = 0, nkv = (a.k_len + TK - 1) / TK;
+  if (part) {
+    const int per = (nkv + a.split - 1) / a.split, s = (bid - a.nmain) % a.split;
+    t0 = min(s * per, nkv);
+    nkv = min(nkv, t0 + per) - t0;
+  }
+  // LDS read offsets: K rows, step s (32 d) = chunk 2s + hh; V^T rows, step ks (64 keys) =
+  // chunks 4ks + 2hh, 4ks + 2hh + 1
+  int koff[4], voff[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = f8swz(l32, 2 * s + hh);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) voff[s][c] = SV + f8swz(l32, 4 * s + 2 * hh + c);
+  // DMA: wave w owns 1-KiB pieces 2w, 2w+1 (rows 8p .. 8p+7) of the K and of the V^T image
+  uint32_t vok[2], vov[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (2 * w + i) * 8 + (lane >> 3), pc = lane & 7;
+    const int sw = (pc ^ ((row >> 1) & 7)) << 4;
+    vok[i] = (uint32_t)(row * ld8) + sw;
+    vov[i] = (uint32_t)(row * f.lkp) + sw;
+  }
+  auto dma = [&](int t, int st) {
+    char* Ks = smem + st * SB;
+    char* Vs = Ks + SV;
+    const int tg = t0 + t;
+    const int rows = min(a.Lk - tg * TK, TK);
+    const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * ld8, (uint32_t)(rows * ld8));
+    const i32x4 sv = make_srd(Vb + (int64_t)tg * TK, (uint32_t)(127 * f.lkp + TK));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      dma16_buf(sk, vok[i], 0, lds_addr(Ks + (2 * w + i) * 1024));
+      dma16_buf(sv, vov[i], 0, lds_addr(Vs + (2 * w + i) * 1024));
+    }
+  };
+  auto bar = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if (nkv > 0) dma(0, 0);
+  if (nkv > 1) dma(1, 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+  bar();
+  if (gp == 1) {
+    __builtin_amdgcn_s_setprio(1);
+    bar();
+  }
+
+  i32x16 si[4];
+  f32x16 s[4];
+  i32x8 pf[2];
+  int st = 0, stp = 2;
+  for (int t = 0; t <= nkv; ++t) {
+    // ---------------- X_t ----------------
+    if (t < nkv) {
+      const char* Ks = smem + st * SB;
+      i32x4 qf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const i32x4*)(Qs + koff[ks]);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[0]), qf[0], (i32x16){});
+#pragma unroll
+        for (int ks = 1; ks < 4; ++ks)
+          si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[ks]), qf[ks], si[kt]);
+      }
+      if (SCHED) {
+        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 5, 0);
+#pragma unroll
+        for (int i = 0; i < 16 - 1 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
+      }
+    }
+    if (t > 0) {
+      const char* Vs = smem + stp * SB;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const i32x4 lo = *(const i32x4*)(Vs + dt * 4096 + voff[ks][0]);
+          const i32x4 hi = *(const i32x4*)(Vs + dt * 4096 + voff[ks][1]);
+          o[dt] = mfma8(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), pf[ks], o[dt]);
+        }
+        if (ATTN_LP_SUM_MFMA) o[NO - 1] = mfma8(ones, pf[ks], o[NO - 1]);
+      }
+    }
+    if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    // ---------------- Y_t ----------------
+    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
+    if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+    if (t < nkv) {
+      const int kbase = (t0 + t) * TK;
+      const float c = cq * skb[t0 + t];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kt][r] = (float)si[kt][r];
+      if (kbase + TK > a.k_len) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kbase + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) s[kt][r] = NEG_INF;
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+      mx = xhalf_max(mx);
+      const float mnew = fmaxf(m, mx * c);
+      if (__any(mnew > m + TAU)) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        lsum *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < NO; ++dt) o[dt] *= alpha;
+        m = mnew;
+        mb = m - OFF;
+      }
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] * c - mb);
+          if (!ATTN_LP_SUM_MFMA) lsum += s[kt][r];
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int d4 = 0; d4 < 8; ++d4) {
+          const f32x16& x = s[2 * ks + (d4 >> 2)];
+          const int r = 4 * (d4 & 3);
+          pf[ks][d4] = (int)cvt4_fp8(x[r], x[r + 1], x[r + 2], x[r + 3]);
+        }
+    }
+    if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    stp = st;
+    st = st == 2 ? 0 : st + 1;
+  }
+  if (gp == 0) bar();
+  if (clk) {
+    const unsigned long long c1 = clock64(), w1 = wall_clock64();
+    a.clk[0] = c1 - c0;
+    a.clk[1] = w1 - w0;
+  }
+  if (ATTN_LP_SUM_MFMA)
+    lsum = o[NO - 1][0];         // row sums (every row of the fifth O^T tile)
+  else
+    lsum += __shfl_xor(lsum, 32, 64);
+  const int qr = q0 + w * 32 + l32;
+  const unsigned* vam = f.vamax + ((int64_t)b * a.H + h) * HD;
+  if (part) {
+    const int j = bid - a.nmain, row = w * 32 + l32;
+    float* Op = a.Opart + ((int64_t)j * 256 + row) * HD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int d = dt * 32 + 8 * rg + 4 * hh;
+        const f32x4 sv = __builtin_bit_cast(f32x4, *(const u32x4*)(vam + d)) * (1.f / FP8_QMAX);
+        *(f32x4*)(Op + d) = (f32x4){o[dt][rg * 4], o[dt][rg * 4 + 1], o[dt][rg * 4 + 2],
+                                    o[dt][rg * 4 + 3]} * sv;
+      }
+    if (hh == 0) *(f32x2*)(a.MLpart + ((int64_t)j * 256 + row) * 2) = (f32x2){mb, lsum};
+  } else if (qr < a.Lq) {
+    bf16* Ob = a.O + b * a.bo + h * HD + (int64_t)qr * a.ldo;
+    const float inv = 1.f / lsum;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int d = dt * 32 + 8 * rg + 4 * hh;
+        const f32x4 sv = __builtin_bit_cast(f32x4, *(const u32x4*)(vam + d)) * (inv / FP8_QMAX);
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][rg * 4 + r] * sv[r]);
+        *(bf16x4*)(Ob + d) = v;
+      }
+    if (hh == 0) a.LSE[((int64_t)b * a.H + h) * a.Lq + qr] = mb + log2f(lsum);
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Split-KV tail of the long-KV forward.  One workgroup per CU (144 KiB of LDS), so the grid
@@ -898,12 +1331,12 @@ int64_t tail_units(int64_t nunits, int64_t nwork, int& nmain, int& split) {
 
 // forward (long KV only): units = query tiles, work = 96-key tiles; workspace bytes
 int64_t tail_split(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, int& nmain,
-                   int& split) {
+                   int& split, int64_t tk = 96) {
   const int64_t units = ((Lq + 255) / 256) * H * B;
   nmain = (int)units;
   split = 1;
   if (Lk < 4096) return 0;
-  const int64_t rem = tail_units(units, (k_len + 95) / 96, nmain, split);
+  const int64_t rem = tail_units(units, (k_len + tk - 1) / tk, nmain, split);
   return rem * split * 256 * (HD * 4 + 8);
 }
 
@@ -977,6 +1410,90 @@ extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void*
                              int64_t Lk, int64_t H, int64_t k_len, float scale, void* stream) {
   return prfl_attn_fwd_ws(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H,
                           k_len, scale, nullptr, 0, stream);
+}
+
+// ---- low-precision forward (C5) -----------------------------------------------------------
+namespace {
+constexpr int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+struct LpLayout {
+  int64_t vam, sq, sk, q8, k8, vt8, tail, total, lkp;
+};
+LpLayout lp_layout(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, int& nmain,
+                   int& split) {
+  LpLayout l;
+  l.lkp = (Lk + 127) / 128 * 128;
+  l.vam = 0;
+  l.sq = l.vam + al256(B * H * HD * 4);
+  l.sk = l.sq + al256(B * H * Lq * 4);
+  l.q8 = l.sk + al256(B * H * (l.lkp / 128) * 4);
+  l.k8 = l.q8 + al256(B * Lq * H * HD);
+  l.vt8 = l.k8 + al256(B * Lk * H * HD);
+  l.tail = l.vt8 + al256(B * H * HD * l.lkp);
+  l.total = l.tail + tail_split(B, Lq, Lk, H, k_len, nmain, split, 128);
+  return l;
+}
+}  // namespace
+
+extern "C" int64_t prfl_attn_fwd_fp8_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                                              int64_t k_len) {
+  int nmain, split;
+  if (B <= 0 || Lq <= 0 || H <= 0 || Lk <= 0) return 0;
+  return lp_layout(B, Lq, Lk, H, k_len, nmain, split).total;
+}
+
+// prfl_attn_fwd_ws at twice the bf16 MFMA rate (config C5; S on the int8 MFMA, P.V on the e4m3
+// MFMA, see attn_fwd_lp_kernel): q, k, v bf16 in the same layout, quantised into the
+// caller-owned workspace ws (prfl_attn_fwd_fp8_ws_bytes(...) bytes, 256-B aligned, required) by
+// two prologue kernels; o / lse2 as the bf16 forward's (lse2 is the log2-domain LSE of the
+// dequantised scores, so the bf16 backward can use it).
+extern "C" int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                 int64_t ldk, int64_t bk, const void* v, int64_t ldv, int64_t bv,
+                                 void* o, int64_t ldo, int64_t bo, float* lse2, int64_t B,
+                                 int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, float scale,
+                                 void* ws, int64_t ws_bytes, void* stream) {
+  if (B <= 0 || Lq <= 0 || H <= 0) return 0;
+  if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !ws ||
+      ((uintptr_t)ws & 255) || (ldq | ldk | ldv | ldo) % 8)
+    return (int)hipErrorInvalidValue;
+  const int64_t lkp = (Lk + 127) / 128 * 128;
+  if (Lq > 0x7fffffff || Lk > 0x7fffffff || H > 65535 || B > 65535 ||
+      ((Lq + 255) / 256) * H * B > 0x7fffffff || (int64_t)127 * lkp + 128 > 0xffffffffLL ||
+      (int64_t)128 * H * HD > 0xffffffffLL)
+    return (int)hipErrorInvalidValue;
+  int nmain, split;
+  const LpLayout l = lp_layout(B, Lq, Lk, H, k_len, nmain, split);
+  if (ws_bytes < l.total) return (int)hipErrorInvalidValue;
+  char* w = (char*)ws;
+  const int64_t nwg = ((Lq + 255) / 256) * H * B, rem = nwg - nmain;
+  float* Opart = (float*)(w + l.tail);
+  float* MLpart = split > 1 ? Opart + rem * split * 256 * HD : nullptr;
+  AttnF8Args f{{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
+                (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
+                scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart, nullptr},
+               (const int8_t*)(w + l.q8), (const float*)(w + l.sq), (const int8_t*)(w + l.k8),
+               (const float*)(w + l.sk), (const uint8_t*)(w + l.vt8),
+               (const unsigned*)(w + l.vam), l.lkp};
+  hipStream_t s = (hipStream_t)stream;
+  prfl_prof::begin(KID_ELTWISE, s);
+  if (hipMemsetAsync(w + l.vam, 0, B * H * HD * 4, s) != hipSuccess) return (int)hipErrorLaunchFailure;
+  hipLaunchKernelGGL(attn_lp_vamax_kernel, dim3((unsigned)((Lk + 255) / 256), (unsigned)H, (unsigned)B),
+                     dim3(256), 0, s, f);
+  hipLaunchKernelGGL(attn_lp_quant_kernel,
+                     dim3((unsigned)((std::max(Lq, lkp) + 127) / 128), (unsigned)H, (unsigned)B),
+                     dim3(256), 0, s, f);
+  prfl_prof::set_work((double)B * H * HD * (3.0 * Lq + 7.0 * Lk + lkp));   // bytes moved
+  prfl_prof::end(KID_ELTWISE, s);
+  PRFL_LAUNCH_CHECK();
+  prfl_prof::begin(KID_ATTN_FWD_FP8, s);
+  f.base.clk = prfl_prof::clk_slot();
+  hipLaunchKernelGGL(attn_fwd_lp_kernel<ATTN_LP_SCHED>, dim3((unsigned)(nmain + rem * split)),
+                     dim3(512), 0, s, f);
+  if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem, 8), dim3(256), 0, s, f.base);
+  prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
+  prfl_prof::end(KID_ATTN_FWD_FP8, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
 }
 
 // dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace; ws: caller-owned

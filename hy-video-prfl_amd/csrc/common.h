@@ -189,6 +189,6 @@ unsigned long long* clk_slot();  // (cycles, 100 MHz ticks) slot for the next la
 }
 enum {
   KID_GEMM = 0, KID_ATTN_FWD, KID_ATTN_FWD_SHORT, KID_ATTN_BWD_DKDV, KID_ATTN_BWD_DQ, KID_LN, KID_RMS,
-  KID_ELTWISE, KID_ADAMW, KID_POOL,
+  KID_ELTWISE, KID_ADAMW, KID_POOL, KID_ATTN_FWD_FP8,
   KID_COUNT
 };

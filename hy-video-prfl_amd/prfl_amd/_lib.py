@@ -26,6 +26,9 @@ SIGNATURES = {
     "prfl_attn_fwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
                          I64, F32, P, I64, P],
     "prfl_attn_fwd_ws_bytes": [I64, I64, I64, I64, I64],
+    "prfl_attn_fwd_fp8": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
+                          I64, I64, F32, P, I64, P],
+    "prfl_attn_fwd_fp8_ws_bytes": [I64, I64, I64, I64, I64],
     "prfl_attn_bwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P,
                          I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, I64,
                          P],
@@ -61,12 +64,12 @@ SIGNATURES = {
 }
 
 # entries that return a value other than a hipError_t code
-RESTYPES = {"prfl_attn_fwd_ws_bytes": I64, "prfl_attn_bwd_ws_bytes": I64}
+RESTYPES = {"prfl_attn_fwd_ws_bytes": I64, "prfl_attn_fwd_fp8_ws_bytes": I64, "prfl_attn_bwd_ws_bytes": I64}
 
 # kernel ids of the profiling hooks (csrc/common.h)
 KID = dict(gemm=0, attn_fwd=1, attn_fwd_short=2, attn_bwd_dkdv=3, attn_bwd_dq=4, ln=5, rms=6,
-           eltwise=7, adamw=8, pool=9)
-NKID = 10
+           eltwise=7, adamw=8, pool=9, attn_fwd_fp8=10)
+NKID = 11
 
 _lib = None
 

@@ -68,9 +68,11 @@ def credit_attn_stash(nbytes):
 class Meta:
     """Non-tensor block arguments."""
 
-    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6, fp8=False):
+    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6, fp8=0):
         self.num_heads = num_heads
-        self.fp8 = fp8              # config C5: fp8 forward projections (WanModel.set_fp8_gemm)
+        # config C5 (WanModel.set_fp8_gemm): 0 bf16; 1 e4m3 forward projections; 2 also the e4m3
+        # self-attention forward (ops.attn_fwd_fp8; its backward stays bf16 on that forward's O/LSE)
+        self.fp8 = int(fp8)
         self.grid = grid            # list of (F, H, W) per sample
         self.seq_len = seq_len      # list of valid key lengths per sample (k_lens)
         self.rope_tab = rope_tab    # fp32 [1024, 64, 2] device tensor
@@ -160,7 +162,11 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False
     grid = meta.grid[b]
     qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid)
     kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
-    ao, lse = attn if attn is not None else ops.attn_fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
+    if attn is not None:
+        ao, lse = attn
+    else:
+        fwd = ops.attn_fwd_fp8 if meta.fp8 >= 2 else ops.attn_fwd
+        ao, lse = fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
     if keep_attn:
         S["attn"] = (ao, lse)
     y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
@@ -344,5 +350,5 @@ def block_apply(P, x, e, context, meta, allow_keep=True):
     grid = [int(v) for g in meta.grid for v in g]
     out, _, _ = custom_ops.wan_block(x, e, context, params, int(meta.num_heads), grid,
                                      [int(v) for v in meta.seq_len], meta.rope_tab, bool(meta.i2v),
-                                     float(meta.eps), bool(meta.fp8), keep)
+                                     float(meta.eps), int(meta.fp8), keep)
     return out

@@ -44,14 +44,15 @@ def _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8):
 @torch.library.custom_op("prfl::wan_block", mutates_args=(), device_types="cuda")
 def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_heads: int,
               grid: List[int], seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float,
-              fp8: bool, keep_attn: bool) -> Tuple[Tensor, Tensor, Tensor]:
-    """x [B, L, C] (fp32, or bf16 for block 0), e [B, 6, C] fp32 (modulation + e0), context
+              fp8: int, keep_attn: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    """fp8: 0 bf16, 1 e4m3 forward projections, 2 also the e4m3 self-attention forward
+    (config C5, block.Meta).  x [B, L, C] (fp32, or bf16 for block 0), e [B, 6, C] fp32 (modulation + e0), context
     [B, Lc, C] bf16, params in block.param_names(i2v) order, grid = flattened (F, H, W) per
     sample.  Returns (out fp32 [B, L, C], kept self-attention output bf16 [B, L, C] and LSE fp32
     [B, H, L] when keep_attn, else empty)."""
     meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8)
     P = dict(zip(B.param_names(i2v), params))
-    W = B.BF16Weights(P, fp8=fp8, need_bf16=False)
+    W = B.BF16Weights(P, fp8=fp8 > 0, need_bf16=False)
     outs, aos, lses = [], [], []
     for b in range(x.shape[0]):
         o, S = B.block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False,
@@ -78,7 +79,7 @@ def _(x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8,
 @torch.library.custom_op("prfl::wan_block_backward", mutates_args=(), device_types="cuda")
 def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, params: List[Tensor],
                        ao: Tensor, lse: Tensor, num_heads: int, grid: List[int],
-                       seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float, fp8: bool,
+                       seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float, fp8: int,
                        want_w: bool, want_ctx: bool) -> List[Tensor]:
     """Recompute the block forward (reusing a kept (ao, lse) when given), then the backward
     chain.  Returns [dx (x.dtype), de fp32, dctx (context.dtype or empty), *dparams (param
@@ -86,7 +87,7 @@ def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, para
     meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8)
     names = B.param_names(i2v)
     P = dict(zip(names, params))
-    W = B.BF16Weights(P, fp8=fp8)
+    W = B.BF16Weights(P, fp8=fp8 > 0)
     G = {}
     dxs, des, dcs = [], [], []
     kept = ao.numel() > 0

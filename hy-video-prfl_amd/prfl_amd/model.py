@@ -175,7 +175,7 @@ def _rope_table(freqs, device):
 class WanAttentionBlock(nn.Module):
     """model.py:280-359.  forward() is one fused, activation-checkpointed HIP autograd node."""
 
-    fp8_gemm = False    # config C5's fp8 path (WanModel.set_fp8_gemm); the reference is bf16-only
+    fp8_gemm = 0        # config C5's fp8 path (WanModel.set_fp8_gemm); the reference is bf16-only
     self_checkpointing = True   # forward is already the per-block checkpoint (fsdp_utils.py)
     stash_attn = True           # may keep its attention output for the backward (block.py)
 
@@ -306,13 +306,14 @@ class WanModel(nn.Module):
             self.img_emb = MLPProj(1280, dim, flf_pos_emb=model_type == "flf2v")
         self.init_weights()
 
-    def set_fp8_gemm(self, on=True):
+    def set_fp8_gemm(self, on=True, attn=False):
         """Config C5 (`train_prfl_i2v_720`, "fp8 MFMA path"): every block's large forward
         projections — QKV, self-attn O, cross-attn q/o, FFN in/out — run as per-row e4m3 operands
-        on the block-scaled fp8 MFMA; the backward GEMMs stay bf16 (straight-through).  Held to
-        SURVEY §8c's 5e-2 against the bf16 path, not to the reference (which is bf16-only)."""
+        on the block-scaled fp8 MFMA; the backward GEMMs stay bf16 (straight-through).  With
+        `attn` the L x L self-attention forward runs on the e4m3 MFMA too (ops.attn_fwd_fp8).
+        Held to an fp32 truth (k x the bf16 path's error), not to the reference (bf16-only)."""
         for blk in self.blocks:
-            blk.fp8_gemm = bool(on)
+            blk.fp8_gemm = (2 if attn else 1) if on else 0
         return self
 
     # ---------------------------------------------------------------- checkpoint I/O --------

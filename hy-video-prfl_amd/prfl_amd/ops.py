@@ -227,6 +227,25 @@ def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None):
     return out, lse
 
 
+def attn_fwd_fp8(q, k, v, num_heads, k_len=None, out=None, scale=None):
+    """attn_fwd on the block-scaled e4m3 MFMA (config C5 self-attention): same arguments and
+    outputs; q/k/v are quantised inside the call into a scratch buffer (~3 bytes per element)."""
+    Lq, C = q.shape
+    Lk = k.shape[0]
+    assert C == num_heads * 128, "head_dim must be 128"
+    k_len = Lk if k_len is None else int(k_len)
+    sc = scale if scale is not None else 1.0 / math.sqrt(128)
+    if out is None:
+        out = torch.empty(Lq, C, dtype=BF16, device=q.device)
+    lse = torch.empty(num_heads, Lq, dtype=torch.float32, device=q.device)
+    nb = _lib.load().prfl_attn_fwd_fp8_ws_bytes(1, Lq, Lk, num_heads, k_len)
+    ws = torch.empty(nb, dtype=torch.uint8, device=q.device)
+    call("prfl_attn_fwd_fp8", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
+         I64(_ld(v)), I64(0), ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq),
+         I64(Lk), I64(num_heads), I64(k_len), F32(sc), ptr(ws), I64(nb), stream_ptr())
+    return out, lse
+
+
 def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=None, scale=None):
     Lq, C = q.shape
     Lk = k.shape[0]

@@ -74,6 +74,17 @@ int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int6
                      int64_t k_len, float scale, void* ws, int64_t ws_bytes, void* stream);
 /* Scratch bytes prfl_attn_fwd_ws needs on the current device (0 = no split for this shape). */
 int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
+/* Config C5 (fp8): the same forward on the block-scaled e4m3 MFMA.  q, k, v stay bf16 in the
+ * layout above and are quantised inside the call (Q per token and head, K per head, V per head
+ * and channel, V stored transposed) into the REQUIRED caller-owned scratch `ws` (256-B aligned)
+ * of prfl_attn_fwd_fp8_ws_bytes(...) bytes; o and lse2 as prfl_attn_fwd_ws (lse2 is the LSE of
+ * the dequantised scores, usable by prfl_attn_bwd).  There is no fp8 flash-attn in the
+ * reference: its attention stays bf16 (attention.py:113-127) and fp8 covers its linears. */
+int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                      int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
+                      int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                      int64_t k_len, float scale, void* ws, int64_t ws_bytes, void* stream);
+int64_t prfl_attn_fwd_fp8_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
 /* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
  * caller-owned workspace. */
 int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,

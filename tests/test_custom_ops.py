@@ -46,14 +46,14 @@ def test_fake_shapes(cops):
         params = [torch.empty(shapes[n], device=dev) for n in param_names(False)]
         tab = torch.empty(1024, 64, 2, device=dev)
         out, ao, lse = torch.ops.prfl.wan_block(x, e, ctx, params, 2, [3, 5, 7], [105], tab,
-                                                False, 1e-6, False, True)
+                                                False, 1e-6, 0, True)
         assert out.shape == (1, 105, 256) and out.dtype == torch.float32
         assert ao.shape == (1, 105, 256) and ao.dtype == torch.bfloat16 and lse.shape == (1, 2, 105)
         _, ao0, _ = torch.ops.prfl.wan_block(x, e, ctx, params, 2, [3, 5, 7], [105], tab, False,
-                                             1e-6, False, False)
+                                             1e-6, 0, False)
         assert ao0.numel() == 0
         g = torch.ops.prfl.wan_block_backward(out, x, e, ctx, params, ao, lse, 2, [3, 5, 7], [105],
-                                              tab, False, 1e-6, False, True, True)
+                                              tab, False, 1e-6, 0, True, True)
         assert [t.shape for t in g[3:]] == [p.shape for p in params] and g[2].shape == ctx.shape
         o, l2, o32 = torch.ops.prfl.query_pool(torch.empty(2, 5120, device=dev, dtype=torch.bfloat16),
                                           torch.empty(2, 77, 10240, device=dev, dtype=torch.bfloat16),

@@ -64,7 +64,7 @@ def test_opcheck_wan_block(cops):
     x, e, ctx, params, tab = _block_inputs()
     for keep in (False, True):
         torch.library.opcheck(torch.ops.prfl.wan_block.default,
-                              (x, e, ctx, params, 2, [3, 5, 7], [105], tab, False, 1e-6, False, keep),
+                              (x, e, ctx, params, 2, [3, 5, 7], [105], tab, False, 1e-6, 0, keep),
                               test_utils=OPCHECK)
 
 

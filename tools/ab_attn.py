@@ -25,6 +25,10 @@ def load(path):
         lib.prfl_attn_fwd_ws.argtypes, lib.prfl_attn_fwd_ws.restype = FWD[:-1] + [P, I64, P], ctypes.c_int
         lib.prfl_attn_fwd_ws_bytes.argtypes = [I64] * 5
         lib.prfl_attn_fwd_ws_bytes.restype = I64
+    if hasattr(lib, "prfl_attn_fwd_fp8"):
+        lib.prfl_attn_fwd_fp8.argtypes, lib.prfl_attn_fwd_fp8.restype = FWD[:-1] + [P, I64, P], ctypes.c_int
+        lib.prfl_attn_fwd_fp8_ws_bytes.argtypes = [I64] * 5
+        lib.prfl_attn_fwd_fp8_ws_bytes.restype = I64
     lib.has_bws = hasattr(lib, "prfl_attn_bwd_ws")
     if lib.has_bws:
         lib.prfl_attn_bwd_ws.argtypes, lib.prfl_attn_bwd_ws.restype = BWD[:-1] + [P, I64, P], ctypes.c_int

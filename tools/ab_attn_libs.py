@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--L", type=int, default=73920)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="time prfl_attn_fwd_fp8 (config C5) instead")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     L, H, C = a.L, 40, 5120
@@ -34,7 +35,12 @@ def main():
     def fwd(lib, b):
         args = (q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
                 b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc)
-        if lib.has_ws:
+        if a.fp8:
+            nb = lib.prfl_attn_fwd_fp8_ws_bytes(1, L, L, H, L)
+            if "ws8" not in b or b["ws8"].numel() < nb:
+                b["ws8"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+            assert lib.prfl_attn_fwd_fp8(*args, b["ws8"].data_ptr(), nb, st) == 0
+        elif lib.has_ws:
             nb = lib.prfl_attn_fwd_ws_bytes(1, L, L, H, L)
             if "ws" not in b or b["ws"].numel() < nb:
                 b["ws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
