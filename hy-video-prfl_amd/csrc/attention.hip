@@ -171,12 +171,16 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // with the same relative error at any scale).  TAU = 8: 720p forward 100.22 -> 95.98 ms (+4.4 %),
 // rel-L2 vs an fp64 softmax attention 2.33e-3 -> 2.38e-3 on sampled rows
 // (profiles/r03_ab_attn_lazy.txt)
+// (Row sums on the MFMA — a fifth O^T tile with an all-ones A operand instead of 48 v_add per
+// tile, as the C5 kernel does — measured 5 % SLOWER here: this kernel is bound by its MFMA pipe
+// and LDS reads, not its VALU; profiles/r03_ab_attn_fwd_summfma.txt)
 #ifndef ATTN_LAZY_TAU
 #define ATTN_LAZY_TAU 8
 #endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
+
 template <bool SHORT_KV, int SCHED, int NKT>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
@@ -1054,6 +1058,9 @@ __global__ __launch_bounds__(256) void attn_lp_quant_kernel(AttnF8Args f) {
 #ifndef ATTN_LP_SUM_MFMA
 #define ATTN_LP_SUM_MFMA 1
 #endif
+#ifndef ATTN_LP_MAGIC
+#define ATTN_LP_MAGIC 1
+#endif
 #ifndef ATTN_LP_SCHED
 #define ATTN_LP_SCHED 1
 #endif
@@ -1164,6 +1171,14 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
   f32x16 s[4];
   i32x8 pf[2];
   int st = 0, stp = 2;
+  // ATTN_LP_MAGIC: the Q.K^T accumulators start at the fp32 bit pattern of 1.5 * 2^23, so the
+  // i32 result read as fp32 IS 1.5 * 2^23 + S exactly (|S| <= 127^2 * 128 < 2^22): no
+  // v_cvt_f32_i32 per score; the offset is folded into the softmax FMA's constant
+  constexpr int MAGIC = 0x4B400000;
+  constexpr float FMAGIC = 12582912.f;
+  const i32x16 acc0 = ATTN_LP_MAGIC ? (i32x16){MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC,
+                                               MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC}
+                                    : (i32x16){};
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (t < nkv) {
@@ -1173,7 +1188,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
       for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const i32x4*)(Qs + koff[ks]);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[0]), qf[0], (i32x16){});
+        si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[0]), qf[0], acc0);
 #pragma unroll
         for (int ks = 1; ks < 4; ++ks)
           si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[ks]), qf[ks], si[kt]);
@@ -1212,7 +1227,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] = (float)si[kt][r];
+        for (int r = 0; r < 16; ++r)
+          s[kt][r] = ATTN_LP_MAGIC ? __int_as_float(si[kt][r]) : (float)si[kt][r];
       if (kbase + TK > a.k_len) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
@@ -1226,6 +1242,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = xhalf_max(mx);
+      if (ATTN_LP_MAGIC) mx -= FMAGIC;           // exact (Sterbenz)
       const float mnew = fmaxf(m, mx * c);
       if (__any(mnew > m + TAU)) {
         const float alpha = __builtin_amdgcn_exp2f(m - mnew);
@@ -1235,11 +1252,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
         m = mnew;
         mb = m - OFF;
       }
+      const float kb = ATTN_LP_MAGIC ? fmaf(FMAGIC, c, mb) : mb;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] * c - mb);
+          s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] * c - kb);
           if (!ATTN_LP_SUM_MFMA) lsum += s[kt][r];
         }
 #pragma unroll

@@ -160,7 +160,9 @@ def test_block_fp8_vs_fp32_truth():
     block (GPU run r3a): 4.5x (dx) to 9.8x (FFN-out weight grad), update 8.4x = 5.3 % vs 0.62 %
     — the e4m3 mantissa, not the kernel: per-row scales leave no operand subnormal, so block
     scaling cannot lower it.  A broken fp8 kernel (wrong scale, lost k-block) is >= 100 % off,
-    > 160x.  The bf16 path itself is also held to the oracle (<= 1e-2)."""
+    > 160x.  The bf16 path itself is also held to the oracle (<= 1e-2).  The same bound holds with
+    the C5 self-attention forward (int8 Q.K^T, e4m3 P.V) on as well (block.Meta fp8 = 2):
+    measured within 5 % of the projections-only errors on every tensor (GPU run r3i)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
@@ -216,7 +218,7 @@ def test_block_fp8_vs_fp32_truth():
     print("fp8+attn / bf16    ", {k: round(e8a[k] / e16[k], 2) for k in keys})
     for k in keys:
         assert e8[k] <= 16 * e16[k] and e8[k] <= 1e-1, (k, e8[k], e16[k])
-        assert e8a[k] <= 32 * e16[k] and e8a[k] <= 1.5e-1, (k, e8a[k], e16[k])
+        assert e8a[k] <= 16 * e16[k] and e8a[k] <= 1e-1, (k, e8a[k], e16[k])
     assert e16_vs_oracle["update"] < 1e-2 and e16_vs_oracle["dx"] < 3e-2, e16_vs_oracle
 
 
@@ -264,8 +266,11 @@ def test_attn_fp8_vs_dequantised_fp64(Lq, Lk, H, klen):
     products, the transposed and key-permuted V image, the folded per-token / per-tile / per-
     channel scales, masking, the split-KV tail: 4200 x 16 heads = 272 query-tile units on 256
     CUs) from the rounding of Q, K, V itself.  Left: the e4m3 rounding of P and fp32
-    accumulation: O within 2.5e-2 rel-L2 (a swapped key or channel is ~1.4); the scores are exact
-    (integer products, i32 sums), so the log2 LSE is within 1e-3."""
+    accumulation: O within 2.5e-2 rel-L2 (measured 1.7-2.0e-2; a swapped key or channel is
+    ~1.4).  The scores are exact (integer products, i32 sums), but the row sums come out of the
+    P.V MFMA over the e4m3-ROUNDED P (the normaliser then matches the numerator's weights), so the
+    log2 LSE carries that rounding: within 5e-2 (measured <= 2.7e-2, i.e. <= 1.9 % in the sum;
+    a lost key tile or a wrong scale is >= 1)."""
     from prfl_amd import ops
     g = torch.Generator(device=DEV).manual_seed(Lq * 7 + Lk)
     C = H * 128
@@ -282,15 +287,19 @@ def test_attn_fp8_vs_dequantised_fp64(Lq, Lk, H, klen):
     r = rel(o, ro)
     print(f"vs dequantised fp64: O rel-L2 {r:.3e}, max |dLSE2| {(lse.double() - rlse).abs().max().item():.2e}")
     assert r < 2.5e-2, r
-    assert (lse.double() - rlse).abs().max().item() < 1e-3
+    assert (lse.double() - rlse).abs().max().item() < 5e-2
 
 
 @pytest.mark.parametrize("L,H", [(4200, 16), (73920, 1)])
 def test_attn_fp8_vs_fp64_truth(L, H):
     """fp32-truth rule of config C5 (as for the fp8 block): err(C5 attention
-    vs fp64 attention of the bf16 operands) <= k * err(bf16 attention vs the same), k = 16 (the
-    e4m3 / bf16 unit-roundoff ratio, see test_block_fp8_vs_fp32_truth), on sampled query rows
-    incl. the 720p x 81f token count (73 920 keys)."""
+    vs fp64 attention of the bf16 operands) <= k * err(bf16 attention vs the same) on sampled
+    query rows, incl. the 720p x 81f token count (73 920 keys).  k = 24: the P.V product rounds
+    BOTH of its operands to e4m3 (P and V, independent roundings, unit roundoff 2^-4 each) where
+    the bf16 kernel rounds one (P, 2^-8): sqrt(2) x 16 = 22.6, rounded up.  Zero-mean random V
+    is the worst case for a relative error (|O| is small while each rounding error is not);
+    measured 17.3x (4 200 keys, 16 heads) and 19.4x (73 920 keys), 4.0-4.4 % vs 0.23 %; the
+    kernel alone against the dequantised operands is test_attn_fp8_vs_dequantised_fp64."""
     from prfl_amd import ops
     g = torch.Generator(device=DEV).manual_seed(L + H)
     C = H * 128
@@ -305,5 +314,5 @@ def test_attn_fp8_vs_fp64_truth(L, H):
                     rows=rows)
     e8, e16 = rel(o8[rows], tr), rel(o16[rows], tr)
     print(f"attn C5 vs truth {e8:.3e}, bf16 vs truth {e16:.3e}, ratio {e8 / e16:.2f}")
-    assert e8 <= 16 * e16, (e8, e16)
-    assert e8 < 5e-2
+    assert e8 <= 24 * e16, (e8, e16)
+    assert e8 < 6e-2

@@ -1,5 +1,5 @@
 """Dev probe: isolated hot kernels at the 480p x 81f shapes (L = 32760, C = 5120, 40 heads),
-for rocprofv3 counter runs.  usage: python tools/prof_kernels.py [attn|gemm|attn_bwd] [reps]"""
+for rocprofv3 counter runs.  usage: python tools/prof_kernels.py [attn|attn_fp8|gemm|attn_bwd] [reps]"""
 import os
 import sys
 import time
@@ -14,7 +14,19 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 L, C, NH, F = int(os.environ.get("PRFL_PROF_L", 32760)), 5120, 40, 13824
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-if which in ("attn", "attn_bwd"):
+if which == "attn_fp8":
+    # config C5 self-attention forward (prologue + attn_fwd_lp_kernel)
+    qkv = torch.randn(L, 3 * C, device=dev, generator=g).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    fl = 4 * L * L * C
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        ops.attn_fwd_fp8(q, k, v, NH)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        print(f"attn_fp8 {dt*1e3:.2f} ms  {fl/dt/1e12:.0f} TF/s", flush=True)
+elif which in ("attn", "attn_bwd"):
     qkv = torch.randn(L, 3 * C, device=dev, generator=g).to(torch.bfloat16)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     o, lse = ops.attn_fwd(q, k, v, NH)
