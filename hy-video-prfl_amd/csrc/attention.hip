@@ -1058,8 +1058,10 @@ __global__ __launch_bounds__(256) void attn_lp_quant_kernel(AttnF8Args f) {
 #ifndef ATTN_LP_SUM_MFMA
 #define ATTN_LP_SUM_MFMA 1
 #endif
-#ifndef ATTN_LP_MAGIC
-#define ATTN_LP_MAGIC 1
+// ATTN_LP_STAGES 4 (both halves issue two tiles ahead, 160 KiB of LDS): 66.29 vs 66.08 ms with 3,
+// bit-identical (profiles/r03_ab_attn_lp_variants.txt): DMA latency does not bound this kernel
+#ifndef ATTN_LP_STAGES
+#define ATTN_LP_STAGES 3
 #endif
 #ifndef ATTN_LP_SCHED
 #define ATTN_LP_SCHED 1
@@ -1072,7 +1074,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
   const float OFF = 8.78135971f - TAU;          // log2(440) - TAU
   // ring of [K | V^T] tiles, then each wave's 32 int8 Q rows (read per tile: the Q fragments
   // would hold 16 VGPRs through the softmax phase)
-  __shared__ __attribute__((aligned(16))) char smem[3 * SB + 8 * 4096];
+  constexpr int NS = ATTN_LP_STAGES;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SB + 8 * 4096];
   const int bid = blockIdx.x;
   const bool part = bid >= a.nmain;
   const int unit = part ? a.nmain + (bid - a.nmain) / a.split : bid;
@@ -1090,7 +1093,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
   const int gp = w >> 2;
   const int l32 = lane & 31, hh = lane >> 5;
   const int64_t ld8 = (int64_t)a.H * HD;
-  char* Qs = smem + 3 * SB + w * 4096;
+  char* Qs = smem + NS * SB + w * 4096;
   const int8_t* Kb = f.K8 + (int64_t)b * a.Lk * ld8 + h * HD;
   const uint8_t* Vb = f.Vt8 + ((int64_t)b * a.H + h) * HD * f.lkp;
   const float* skb = f.sk + ((int64_t)b * a.H + h) * (f.lkp >> 7);
@@ -1170,15 +1173,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
   i32x16 si[4];
   f32x16 s[4];
   i32x8 pf[2];
-  int st = 0, stp = 2;
-  // ATTN_LP_MAGIC: the Q.K^T accumulators start at the fp32 bit pattern of 1.5 * 2^23, so the
-  // i32 result read as fp32 IS 1.5 * 2^23 + S exactly (|S| <= 127^2 * 128 < 2^22): no
-  // v_cvt_f32_i32 per score; the offset is folded into the softmax FMA's constant
-  constexpr int MAGIC = 0x4B400000;
-  constexpr float FMAGIC = 12582912.f;
-  const i32x16 acc0 = ATTN_LP_MAGIC ? (i32x16){MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC,
-                                               MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC, MAGIC}
-                                    : (i32x16){};
+  int st = 0, stp = NS - 1;
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (t < nkv) {
@@ -1188,7 +1183,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
       for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const i32x4*)(Qs + koff[ks]);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[0]), qf[0], acc0);
+        si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[0]), qf[0], (i32x16){});
 #pragma unroll
         for (int ks = 1; ks < 4; ++ks)
           si[kt] = mfmai8(*(const i32x4*)(Ks + kt * 4096 + koff[ks]), qf[ks], si[kt]);
@@ -1219,8 +1214,16 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     // ---------------- Y_t ----------------
-    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
-    if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+    // NS = 3: waves 4-7 issue tile t+2 (into the stage tile t-1 left), waves 0-3 tile t+1, which
+    // must land within this phase; NS = 4: both halves issue tile t+2 (into the stage of t-2),
+    // and waves 0-3 retire it one phase later (vmcnt(4): the 4 pieces just issued stay in flight)
+    const bool iss = t + 2 < nkv;
+    if (NS == 4) {
+      if (iss) dma(t + 2, (st + 2) & 3);
+    } else {
+      if (gp == 1 && iss) dma(t + 2, stp);
+      if (gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+    }
     if (t < nkv) {
       const int kbase = (t0 + t) * TK;
       const float c = cq * skb[t0 + t];
@@ -1228,7 +1231,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          s[kt][r] = ATTN_LP_MAGIC ? __int_as_float(si[kt][r]) : (float)si[kt][r];
+          s[kt][r] = (float)si[kt][r];
       if (kbase + TK > a.k_len) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
@@ -1242,7 +1245,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = xhalf_max(mx);
-      if (ATTN_LP_MAGIC) mx -= FMAGIC;           // exact (Sterbenz)
       const float mnew = fmaxf(m, mx * c);
       if (__any(mnew > m + TAU)) {
         const float alpha = __builtin_amdgcn_exp2f(m - mnew);
@@ -1252,12 +1254,11 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
         m = mnew;
         mb = m - OFF;
       }
-      const float kb = ATTN_LP_MAGIC ? fmaf(FMAGIC, c, mb) : mb;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] * c - kb);
+          s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] * c - mb);
           if (!ATTN_LP_SUM_MFMA) lsum += s[kt][r];
         }
 #pragma unroll
@@ -1269,10 +1270,15 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
           pf[ks][d4] = (int)cvt4_fp8(x[r], x[r + 1], x[r + 2], x[r + 3]);
         }
     }
-    if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (gp == 0) {
+      if (NS == 4 && iss)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     bar();
     stp = st;
-    st = st == 2 ? 0 : st + 1;
+    st = st == NS - 1 ? 0 : st + 1;
   }
   if (gp == 0) bar();
   if (clk) {
