@@ -177,11 +177,14 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_LAZY_TAU
 #define ATTN_LAZY_TAU 8
 #endif
+#ifndef ATTN_PV_FIRST
+#define ATTN_PV_FIRST 0
+#endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
 
-template <bool SHORT_KV, int SCHED, int NKT>
+template <bool SHORT_KV, int SCHED, int NKT, bool QS>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
@@ -223,7 +226,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  // QS: the caller pre-scaled Q by softmax_scale * log2(e) and the S accumulators start from
+  // the running max (negm = -m per lane), so the MFMA yields S * sl2 - m and P = exp2(S') takes
+  // one v_exp per score instead of v_fma + v_exp; negm starts at 0, the first tile sets m
   float m = NEG_INF, lsum = 0.f;
+  f32x16 negm;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negm[r] = 0.f;
   // key tiles [t0, t0 + nkv) of this workgroup
   int t0 = 0, nkv = (a.k_len + TK - 1) / TK;
   if (part) {
@@ -289,11 +298,56 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (!ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+#if ATTN_PV_FIRST
+    if (t > 0) {
+      const char* Vs = smem + stp * SB;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int ro = (kt * 32 + 16 * s2) * 256;
+            const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
+            o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
+          }
+      }
+      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
+#pragma unroll
+        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);   // P(t-1) dies before S(t) is born
     if (t < nkv) {
       const char* Ks = smem + st * SB;
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
-        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], (f32x16){});
+        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], QS ? negm : (f32x16){});
+#pragma unroll
+        for (int ks = 1; ks < 8; ++ks)
+          s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
+      }
+      if (SCHED) {   // K-row reads SCHED+1 MFMAs ahead, one per MFMA gap
+        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 1, 0);
+#pragma unroll
+        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
+      }
+    }
+#else
+    if (t < nkv) {
+      const char* Ks = smem + st * SB;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], QS ? negm : (f32x16){});
 #pragma unroll
         for (int ks = 1; ks < 8; ++ks)
           s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
@@ -331,6 +385,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
+#endif
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     // ---------------- Y_t ----------------
@@ -351,6 +406,43 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
       mx = xhalf_max(mx);
+      if (QS) {         // s = S' = S * sl2 - m already
+        // fresh: no tile of this row processed yet (m = -inf, negm = 0: s = S); m is the same in
+        // both lane halves of a query (their partial row sums are not: one half's can underflow
+        // to 0 when the max sits in the other half, so they cannot mark freshness)
+        const bool fresh = m == NEG_INF;
+        const float d = fresh ? mx : fmaxf(mx, 0.f);   // growth of the row max
+        if (__any(fresh || d > (float)ATTN_LAZY_TAU)) {
+          const float alpha = fresh ? 0.f : __builtin_amdgcn_exp2f(-d);
+          lsum *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+          if (fresh) m = 0.f;
+          m += d;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) negm[r] = -m;
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kt][r] -= d;     // (rare: the row max grew)
+        }
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(s[kt][r]);
+            s[kt][r] = p;
+            lsum += p;
+          }
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
+                                  f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
+                                  f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
+                                  f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+      } else {
       const float mnew = fmaxf(m, mx * a.sl2);
       // rescale only when a row max grew (by more than ATTN_LAZY_TAU, log2 units: until then P
       // is taken against the stale max, <= 2^TAU, and O, l and the LSE stay consistent)
@@ -375,6 +467,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
                                 f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
                                 f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
                                 f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+      }
       }
     }
     if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -429,6 +522,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #define ATTN_BWD_DMA_MID 1
 #endif
 // (720p backward 340.0 -> 332.7 ms, profiles/r03_ab_attn_negd.txt)
+// QS (q in log2 units, the *_l2q entries): the dK/dV kernel's S accumulators start at +LSE with
+// K negated, so exp2(-acc) = exp2(S' - LSE) takes one v_exp (neg source modifier) per score
+// instead of v_fma + v_exp (720p backward A/B: profiles/r03_ab_attn_qs.txt)
 #ifndef ATTN_BWD_NEGD
 #define ATTN_BWD_NEGD 1
 #endif
@@ -462,6 +558,7 @@ __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int
 // 64 queries and their LSE / D rows arrive by LDS-DMA into a 2-stage ring, one barrier per tile:
 // tile t+1 is issued at the top of tile t into the stage tile t-1 used (all waves are past the
 // barrier that ended tile t-1) and retired by vmcnt(0) + the barrier that ends tile t.
+template <bool QS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   constexpr int V_BYTES = 256 * 256, STAGE = 16384 * 2 + 512;
   __shared__ __attribute__((aligned(16))) char smem[V_BYTES + 2 * STAGE];
@@ -486,6 +583,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   bf16x8 kf[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) kf[ks] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ks * 16 + hh * 8);
+  if (QS) {     // -K (exact): S accumulators start at +LSE and yield LSE - S'
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kf[ks] = -kf[ks];
+  }
   char* Vs = smem;
   // V rows of the 256 keys (off16 image, row reads): 64 pieces of 4 rows, 8 per wave
 #pragma unroll
@@ -561,6 +662,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
           for (int r = 0; r < 4; ++r) dpt[rg * 4 + r] = d4[r];
         }
       }
+      if (QS) {      // S accumulators start at the LSE of their query rows
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const f32x4 l4 = *(const f32x4*)(Ls + qt * 32 + 8 * rg + 4 * hh);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sacc[rg * 4 + r] = l4[r];
+        }
+      }
       const int row = qt * 32 + l32;
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -577,7 +686,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]);
+          const float p = QS ? __builtin_amdgcn_exp2f(-sacc[rg * 4 + r])
+                                      : __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]);
           sacc[rg * 4 + r] = p;
           dpt[rg * 4 + r] = ATTN_BWD_NEGD ? p * dpt[rg * 4 + r] : p * (dpt[rg * 4 + r] - d4[r]);
         }
@@ -1386,12 +1496,12 @@ extern "C" int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int
 
 // o = softmax(q k^T * scale, keys >= k_len masked) v ; lse2 = log2-domain row LSE.
 // ws: caller-owned scratch of prfl_attn_fwd_ws_bytes(...) bytes for the split-KV tail, or null
-// (no split).
-extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
-                                int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
-                                int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
-                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
-                                int64_t ws_bytes, void* stream) {
+// (no split).  l2q: q is already in log2 units (q * scale * log2 e; scale unused) -> QS kernels.
+namespace {
+int attn_fwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
+                  const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
+                  float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
+                  float scale, bool l2q, void* ws, int64_t ws_bytes, void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(ws) ||
@@ -1411,21 +1521,50 @@ extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const vo
   float* MLpart = split > 1 ? Opart + rem * split * 256 * HD : nullptr;
   AttnArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
              (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-             scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart, nullptr};
+             l2q ? 1.f : scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart, nullptr};
   hipStream_t s = (hipStream_t)stream;
   const int kid = Lk >= 4096 ? KID_ATTN_FWD : KID_ATTN_FWD_SHORT;
   prfl_prof::begin(kid, s);
   if (kid == KID_ATTN_FWD) a.clk = prfl_prof::clk_slot();
   const dim3 grid((unsigned)(nmain + rem * split));
-  if (kid == KID_ATTN_FWD)
-    hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3>), grid, dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3>), grid, dim3(512), 0, s, a);
+  if (kid == KID_ATTN_FWD) {
+    if (l2q)
+      hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, true>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, false>), grid, dim3(512), 0, s, a);
+  } else {
+    if (l2q)
+      hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3, true>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3, false>), grid, dim3(512), 0, s, a);
+  }
   if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(kid, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+}  // namespace
+
+extern "C" int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                                int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o,
+                                int64_t ldo, int64_t bo, float* lse2, int64_t B, int64_t Lq,
+                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
+                                int64_t ws_bytes, void* stream) {
+  return attn_fwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H, k_len,
+                       scale, false, ws, ws_bytes, stream);
+}
+
+// prfl_attn_fwd_ws with q in log2 units: q = q_orig * softmax_scale * log2(e) (the fused block's
+// RMSNorm+RoPE writes it so), so the kernels take one v_exp per score (no scale FMA); o / lse2
+// are those of prfl_attn_fwd_ws(q_orig, ..., softmax_scale)
+extern "C" int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                    int64_t ldk, int64_t bk, const void* v, int64_t ldv, int64_t bv,
+                                    void* o, int64_t ldo, int64_t bo, float* lse2, int64_t B,
+                                    int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, void* ws,
+                                    int64_t ws_bytes, void* stream) {
+  return attn_fwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H, k_len,
+                       1.f, true, ws, ws_bytes, stream);
 }
 
 extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
@@ -1470,11 +1609,11 @@ extern "C" int64_t prfl_attn_fwd_fp8_ws_bytes(int64_t B, int64_t Lq, int64_t Lk,
 // caller-owned workspace ws (prfl_attn_fwd_fp8_ws_bytes(...) bytes, 256-B aligned, required) by
 // two prologue kernels; o / lse2 as the bf16 forward's (lse2 is the log2-domain LSE of the
 // dequantised scores, so the bf16 backward can use it).
-extern "C" int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k,
-                                 int64_t ldk, int64_t bk, const void* v, int64_t ldv, int64_t bv,
-                                 void* o, int64_t ldo, int64_t bo, float* lse2, int64_t B,
-                                 int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, float scale,
-                                 void* ws, int64_t ws_bytes, void* stream) {
+namespace {
+int attn_fwd_fp8_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                      int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
+                      int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                      int64_t k_len, float sl2, void* ws, int64_t ws_bytes, void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !ws ||
@@ -1494,7 +1633,7 @@ extern "C" int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const v
   float* MLpart = split > 1 ? Opart + rem * split * 256 * HD : nullptr;
   AttnF8Args f{{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
                 (bf16*)o, ldo, bo, lse2, (int)Lq, (int)Lk, (int)H, (int)k_len,
-                scale * 1.4426950408889634f, (int)B, nmain, split, Opart, MLpart, nullptr},
+                sl2, (int)B, nmain, split, Opart, MLpart, nullptr},
                (const int8_t*)(w + l.q8), (const float*)(w + l.sq), (const int8_t*)(w + l.k8),
                (const float*)(w + l.sk), (const uint8_t*)(w + l.vt8),
                (const unsigned*)(w + l.vam), l.lkp};
@@ -1519,17 +1658,37 @@ extern "C" int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const v
   PRFL_LAUNCH_CHECK();
   return 0;
 }
+}  // namespace
+
+extern "C" int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                 int64_t ldk, int64_t bk, const void* v, int64_t ldv, int64_t bv,
+                                 void* o, int64_t ldo, int64_t bo, float* lse2, int64_t B,
+                                 int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, float scale,
+                                 void* ws, int64_t ws_bytes, void* stream) {
+  return attn_fwd_fp8_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H,
+                           k_len, scale * 1.4426950408889634f, ws, ws_bytes, stream);
+}
+
+// prfl_attn_fwd_fp8 with q in log2 units (see prfl_attn_fwd_l2q_ws)
+extern "C" int prfl_attn_fwd_fp8_l2q(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                     int64_t ldk, int64_t bk, const void* v, int64_t ldv,
+                                     int64_t bv, void* o, int64_t ldo, int64_t bo, float* lse2,
+                                     int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
+                                     void* ws, int64_t ws_bytes, void* stream) {
+  return attn_fwd_fp8_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H,
+                           k_len, 1.f, ws, ws_bytes, stream);
+}
 
 // dq, dk, dv of the above; delta is a caller-owned [B][H][Lq] fp32 workspace; ws: caller-owned
 // scratch of prfl_attn_bwd_ws_bytes(...) bytes for the split tails, or null (no split).
-extern "C" int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
-                                int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
-                                int64_t ldo, int64_t bo, const void* dout, int64_t lddo,
-                                int64_t bdo, const float* lse2, float* delta, void* dq,
-                                int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
-                                void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
-                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
-                                int64_t ws_bytes, void* stream) {
+namespace {
+int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
+                  const void* v, int64_t ldv, int64_t bv, const void* o, int64_t ldo, int64_t bo,
+                  const void* dout, int64_t lddo, int64_t bdo, const float* lse2, float* delta,
+                  void* dq, int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
+                  void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq, int64_t Lk,
+                  int64_t H, int64_t k_len, float scale, bool l2q, void* ws, int64_t ws_bytes,
+                  void* stream) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
@@ -1558,10 +1717,13 @@ extern "C" int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const vo
   AttnBwdArgs a{(const bf16*)q, ldq, bq, (const bf16*)k, ldk, bk, (const bf16*)v, ldv, bv,
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
-                scale * 1.4426950408889634f, scale, (int)B, nmain_k, split_k, nmain_q, split_q,
-                Pk, Pv, Pq};
+                l2q ? 1.f : scale * 1.4426950408889634f, l2q ? 0.6931471805599453f : scale,
+                (int)B, nmain_k, split_k, nmain_q, split_q, Pk, Pv, Pq};
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((unsigned)(nmain_k + rk * split_k)), dim3(512), 0, s, a);
+  if (l2q)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, dim3((unsigned)(nmain_k + rk * split_k)), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, dim3((unsigned)(nmain_k + rk * split_k)), dim3(512), 0, s, a);
   if (rk) hipLaunchKernelGGL(attn_merge_kv_kernel, dim3((unsigned)rk, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(8.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
@@ -1573,6 +1735,36 @@ extern "C" int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const vo
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+}  // namespace
+
+extern "C" int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                                int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
+                                int64_t ldo, int64_t bo, const void* dout, int64_t lddo,
+                                int64_t bdo, const float* lse2, float* delta, void* dq,
+                                int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
+                                void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
+                                int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
+                                int64_t ws_bytes, void* stream) {
+  return attn_bwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, dout, lddo, bdo, lse2,
+                       delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
+                       scale, false, ws, ws_bytes, stream);
+}
+
+// prfl_attn_bwd_ws for a q in log2 units (prfl_attn_fwd_l2q_ws): dq is the gradient w.r.t. that
+// pre-scaled q (= ln 2 * dS K; the RMSNorm+RoPE backward multiplies it back by scale * log2 e),
+// dk / dv are those of the unscaled problem
+extern "C" int prfl_attn_bwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                    int64_t ldk, int64_t bk, const void* v, int64_t ldv, int64_t bv,
+                                    const void* o, int64_t ldo, int64_t bo, const void* dout,
+                                    int64_t lddo, int64_t bdo, const float* lse2, float* delta,
+                                    void* dq, int64_t lddq, int64_t bdq, void* dk, int64_t lddk,
+                                    int64_t bdk, void* dv, int64_t lddv, int64_t bdv, int64_t B,
+                                    int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, void* ws,
+                                    int64_t ws_bytes, void* stream) {
+  return attn_bwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, dout, lddo, bdo, lse2,
+                       delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
+                       1.f, true, ws, ws_bytes, stream);
 }
 
 extern "C" int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H,

@@ -95,6 +95,31 @@ __device__ __forceinline__ void dma16_buf(i32x4 srd, uint32_t voff, uint32_t sof
       : "memory");
 }
 
+// Grouped form: m0 set once (saved) for several pieces at consecutive KiB of LDS, each piece then
+// `buffer_load_dwordx4 ... offen offset:PIECE*1024 lds` (the instruction offset adds to both the
+// LDS and the global address: the caller pre-subtracts it from voff), m0 restored after the group.
+__device__ __forceinline__ void m0_set(uint32_t lds_base, unsigned& keep) {
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0"
+               : "=&s"(keep) : "s"(__builtin_amdgcn_readfirstlane(lds_base)) : "memory");
+}
+__device__ __forceinline__ void m0_restore(unsigned keep) {
+  asm volatile("s_mov_b32 m0, %0" :: "s"(keep) : "memory");
+}
+template <int PIECE>
+__device__ __forceinline__ void dma16_buf_m0_(i32x4 srd, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen offset:%3 lds"
+               :: "v"(voff), "s"(srd), "s"(__builtin_amdgcn_readfirstlane(soff)), "i"(PIECE * 1024)
+               : "memory");
+}
+__device__ __forceinline__ void dma16_buf_m0(i32x4 srd, uint32_t voff, uint32_t soff, int piece) {
+  switch (piece) {
+    case 0: dma16_buf_m0_<0>(srd, voff, soff); break;
+    case 1: dma16_buf_m0_<1>(srd, voff, soff); break;
+    case 2: dma16_buf_m0_<2>(srd, voff, soff); break;
+    default: dma16_buf_m0_<3>(srd, voff, soff); break;
+  }
+}
+
 // 4-B-per-lane buffer variant (buffer_load_dword ... lds): lane i lands at lds_dst + 4 i; a lane
 // whose offset is past the SRD's num_records lands 0.
 __device__ __forceinline__ void dma4_buf(i32x4 srd, uint32_t voff, uint32_t lds_dst) {

@@ -296,6 +296,9 @@ constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
 constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
 
 
+#ifndef GEMM_M0_GROUP
+#define GEMM_M0_GROUP 0
+#endif
 #ifndef GEMM_GROUP_M
 #define GEMM_GROUP_M 4        // 256-row blocks walked together per XCD (L2 / MALL reuse of B)
 #endif
@@ -683,6 +686,15 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i);
     offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i);
   }
+#if GEMM_M0_GROUP
+  unsigned m0keep = 0;
+  uint32_t offa_main[4], offb_main[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {       // prologue keeps the per-piece form; the loop's grouped form
+    offa_main[i] = offa[i] - i * 1024;   // adds i KiB back through the instruction offset
+    offb_main[i] = offb[i] - i * 1024;
+  }
+#endif
   // k0 -> soffset: 2 B per k for K-major operands, one row (ld elements) per k for MN-major
   auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
   auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
@@ -714,8 +726,18 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+#if GEMM_M0_GROUP
+      // one m0 per operand: the wave's 4 pieces are consecutive KiB of LDS, piece i at the
+      // instruction offset i KiB (its global offset was pre-compensated in offa / offb)
+      if (i == 0 || i == 4)
+        m0_set(lds_addr(sd + (i ? HALF4 : 0) + wid * 4096), m0keep);
+      if (i < 4) dma16_buf_m0(srd_a, offa_main[i], soff_a(jd), i);
+      else dma16_buf_m0(srd_b, offb_main[i - 4], soff_b(jd), i - 4);
+      if (i == 3 || i == 7) m0_restore(m0keep);
+#else
       if (i < 4) dma16_buf(srd_a, offa[i], soff_a(jd), lds_addr(sd + (wid * 4 + i) * 1024));
       else dma16_buf(srd_b, offb[i - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + i - 4) * 1024));
+#endif
       na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
       nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
 #pragma unroll

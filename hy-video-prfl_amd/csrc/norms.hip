@@ -4,7 +4,10 @@
 //                (`model.py:125-135, 345, 353`); or affine LN y = LN(x)*w+b -> bf16 (norm3, :352)
 //  rms_rope    : WanRMSNorm over all C channels (`model.py:106-122`): n = bf16(x*rsqrt(mean x^2+eps)),
 //                y = n*w, then the 3-D RoPE of `model.py:61-103` (pairs 0..21 rotate with the frame
-//                index, 22..42 with the row, 43..63 with the column) -> bf16 attention operand.
+//                index, 22..42 with the row, 43..63 with the column) -> bf16 attention operand,
+//                times out_scale (1, or softmax_scale * log2 e for a q that the attention kernels
+//                take in log2 units: the *_l2q entries of attention.hip); the backward scales the
+//                incoming gradient by the same out_scale.
 //
 // One workgroup (256 threads) per row (C <= 5120); the forward holds the row in registers, the
 // backward re-reads it from L1/L2 in a second pass instead of spilling.
@@ -123,7 +126,7 @@ __device__ __forceinline__ int rope_index(int pair, int pf, int ph, int pw) {
 __global__ __launch_bounds__(NT) void rms_rope_fwd_kernel(
     const bf16* __restrict__ x, int64_t ldx, int C, const float* __restrict__ w, float eps,
     const float2* __restrict__ tab, int F, int Hg, int Wg, bf16* __restrict__ out, int64_t ldo,
-    float* __restrict__ rstd_out) {
+    float* __restrict__ rstd_out, float oscale) {
   __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   const int nc = C / 4;
@@ -159,12 +162,12 @@ __global__ __launch_bounds__(NT) void rms_rope_fwd_kernel(
           const int pair = (e0 >> 1) + pp;
           const float2 cs = tab[rope_index(pair, pf, ph, pw) * 64 + pair];
           const float a = y[2 * pp], bq = y[2 * pp + 1];
-          o[2 * pp] = f2bf(__fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bq, cs.y)));
-          o[2 * pp + 1] = f2bf(__fadd_rn(__fmul_rn(a, cs.y), __fmul_rn(bq, cs.x)));
+          o[2 * pp] = f2bf(__fmul_rn(__fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bq, cs.y)), oscale));
+          o[2 * pp + 1] = f2bf(__fmul_rn(__fadd_rn(__fmul_rn(a, cs.y), __fmul_rn(bq, cs.x)), oscale));
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(__fmul_rn(y[r], oscale));
       }
       *(bf16x4*)(out + row * ldo + c * 4) = o;
     }
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
     const bf16* __restrict__ dout, int64_t lddo, const bf16* __restrict__ x, int64_t ldx,
     const float* __restrict__ rstd_in, int L, int C, const float* __restrict__ w,
     const float2* __restrict__ tab, int F, int Hg, int Wg, bf16* __restrict__ dx, int64_t lddx,
-    float* __restrict__ part0) {
+    float* __restrict__ part0, float oscale) {
   __shared__ float red[NT / 64];
   const int nc = C / 4;
   f32x4 p0[MAXV];
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
         const int c = threadIdx.x + j * NT;
         if (c < nc) {
           const f32x4 xv = ld4(x, row * ldx + c * 4, 1);
-          const f32x4 gv = ld4(dout, row * lddo + c * 4, 1);
+          const f32x4 gv = ld4(dout, row * lddo + c * 4, 1) * oscale;
           const f32x4 wv = ldf4(w, c * 4);
           float dy[4];
           if (rot) {
@@ -361,13 +364,15 @@ extern "C" int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int 
 
 extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
                                  float eps, const float* rope_tab, int64_t F, int64_t Hg,
-                                 int64_t Wg, void* out, int64_t ldo, float* rstd, void* stream) {
+                                 int64_t Wg, void* out, int64_t ldo, float* rstd, float out_scale,
+                                 void* stream) {
   if (L <= 0) return 0;
   if (bad_c(C)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
   hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C, w,
-                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd);
+                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd,
+                     out_scale);
   prfl_prof::set_work((double)L * C * 4);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();
@@ -377,14 +382,15 @@ extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t 
 extern "C" int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
                                  const float* rstd, int64_t L, int64_t C, const float* w,
                                  const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                                 int64_t lddx, float* part0, void* stream) {
+                                 int64_t lddx, float* part0, float out_scale, void* stream) {
   if (L <= 0) return 0;
   if (bad_c(C)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
   hipLaunchKernelGGL(rms_rope_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
                      0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L, (int)C, w,
-                     (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)dx, lddx, part0);
+                     (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)dx, lddx, part0,
+                     out_scale);
   prfl_prof::set_work((double)L * C * 6);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();

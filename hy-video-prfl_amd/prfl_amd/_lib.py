@@ -26,20 +26,27 @@ SIGNATURES = {
     "prfl_attn_fwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64,
                          I64, F32, P, I64, P],
     "prfl_attn_fwd_ws_bytes": [I64, I64, I64, I64, I64],
+    "prfl_attn_fwd_l2q_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
+                             I64, I64, P, I64, P],
     "prfl_attn_fwd_fp8": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
                           I64, I64, F32, P, I64, P],
     "prfl_attn_fwd_fp8_ws_bytes": [I64, I64, I64, I64, I64],
+    "prfl_attn_fwd_fp8_l2q": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
+                              I64, I64, P, I64, P],
     "prfl_attn_bwd_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P,
                          I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, I64,
                          P],
     "prfl_attn_bwd_ws_bytes": [I64, I64, I64, I64, I64],
+    "prfl_attn_bwd_l2q_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P,
+                             P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, P, I64,
+                             P],
     "prfl_attn_bwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64,
                       I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],
     "prfl_ln_mod_bwd": [P, I64, P, I32, I64, P, P, I64, I64, P, P, P, I64, I32, P, P, P],
     "prfl_norm_rows_per_part": [],
-    "prfl_rms_rope_fwd": [P, I64, I64, I64, P, F32, P, I64, I64, I64, P, I64, P, P],
-    "prfl_rms_rope_bwd": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, P, I64, P, P],
+    "prfl_rms_rope_fwd": [P, I64, I64, I64, P, F32, P, I64, I64, I64, P, I64, P, F32, P],
+    "prfl_rms_rope_bwd": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, P, I64, P, F32, P],
     "prfl_cast_f32_bf16": [P, P, I64, P],
     "prfl_gate_bwd": [P, I64, P, I64, P, I64, I64, P, I64, P, P, P],
     "prfl_colsum_bf16": [P, I64, I64, I64, P, P],

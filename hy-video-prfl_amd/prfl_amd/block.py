@@ -160,13 +160,16 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False
     qkv = lin(W, "qkv", h1)
     q_raw, k_raw, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     grid = meta.grid[b]
-    qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid)
+    # q leaves RMSNorm+RoPE already in log2 units (x softmax_scale * log2 e, one bf16 rounding as
+    # before): the attention kernels then take one v_exp per score (ops.L2Q_SCALE, q_log2)
+    qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid,
+                              out_scale=ops.L2Q_SCALE)
     kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
     if attn is not None:
         ao, lse = attn
     else:
         fwd = ops.attn_fwd_fp8 if meta.fp8 >= 2 else ops.attn_fwd
-        ao, lse = fwd(qr, kr, v, nh, k_len=meta.seq_len[b])
+        ao, lse = fwd(qr, kr, v, nh, k_len=meta.seq_len[b], q_log2=True)
     if keep_attn:
         S["attn"] = (ao, lse)
     y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
@@ -179,17 +182,17 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False
     # ---- cross-attention (model.py:352, :204-271) ----
     n3, m3, r3 = ops.ln_mod_fwd(x1, w=g("norm3.weight"), b=g("norm3.bias"), eps=eps)
     qc_raw = lin(W, "cq", n3)
-    qc, rqc = ops.rms_rope_fwd(qc_raw, g("cross_attn.norm_q.weight"), eps)
+    qc, rqc = ops.rms_rope_fwd(qc_raw, g("cross_attn.norm_q.weight"), eps, out_scale=ops.L2Q_SCALE)
     ctx_t, ctx_i = _split_ctx(ctx, meta.i2v)
     kc_raw = ops.linear(ctx_t, W.wck, W.bck)
     kc, rkc = ops.rms_rope_fwd(kc_raw, g("cross_attn.norm_k.weight"), eps)
     vc = ops.linear(ctx_t, W.wcv, W.bcv)
-    ac, lsec = ops.attn_fwd(qc, kc, vc, nh)
+    ac, lsec = ops.attn_fwd(qc, kc, vc, nh, q_log2=True)
     if meta.i2v:
         ki_raw = ops.linear(ctx_i, W.wck_img, W.bck_img)
         ki, rki = ops.rms_rope_fwd(ki_raw, g("cross_attn.norm_k_img.weight"), eps)
         vi = ops.linear(ctx_i, W.wcv_img, W.bcv_img)
-        ai, lsei = ops.attn_fwd(qc, ki, vi, nh)
+        ai, lsei = ops.attn_fwd(qc, ki, vi, nh, q_log2=True)
         acs = ac + ai          # fp32 sum of two bf16 outputs, rounded once (model.py:269)
     else:
         acs = ac
@@ -259,11 +262,13 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     dac = ops.linear_dx(dyc, W.wco)
     del dyc
     ctx_t, ctx_i = _split_ctx(ctx, meta.i2v)
-    dqc, dkc, dvc = ops.attn_bwd(S["qc"], S["kc"], S["vc"], S["ac"], dac, S["lsec"], nh)
+    dqc, dkc, dvc = ops.attn_bwd(S["qc"], S["kc"], S["vc"], S["ac"], dac, S["lsec"], nh, q_log2=True)
     if meta.i2v:
-        dqi, dki, dvi = ops.attn_bwd(S["qc"], S["ki"], S["vi"], S["ai"], dac, S["lsei"], nh)
+        dqi, dki, dvi = ops.attn_bwd(S["qc"], S["ki"], S["vi"], S["ai"], dac, S["lsei"], nh,
+                                     q_log2=True)
         dqc = dqc + dqi
-    dqc_raw, dnq = ops.rms_rope_bwd(dqc, S["qc_raw"], S["rqc"], g("cross_attn.norm_q.weight"))
+    dqc_raw, dnq = ops.rms_rope_bwd(dqc, S["qc_raw"], S["rqc"], g("cross_attn.norm_q.weight"),
+                                    out_scale=ops.L2Q_SCALE)
     acc("cross_attn.norm_q.weight", dnq)
     dw("cross_attn.q.weight", dqc_raw, S["n3"])
     if want_w:
@@ -308,10 +313,10 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     qkv = S["qkv"]
     dqkv = torch.empty(L, 3 * C, dtype=BF16, device=x.device)
     dqr, dkr, _ = ops.attn_bwd(S["qr"], S["kr"], qkv[:, 2 * C:], S["ao"], dao, S["lse"], nh,
-                               k_len=meta.seq_len[b], dv=dqkv[:, 2 * C:])
+                               k_len=meta.seq_len[b], dv=dqkv[:, 2 * C:], q_log2=True)
     del dao
     _, dnq = ops.rms_rope_bwd(dqr, qkv[:, :C], S["rq"], g("self_attn.norm_q.weight"),
-                              meta.rope_tab, grid, dx=dqkv[:, :C])
+                              meta.rope_tab, grid, dx=dqkv[:, :C], out_scale=ops.L2Q_SCALE)
     _, dnk = ops.rms_rope_bwd(dkr, qkv[:, C:2 * C], S["rk"], g("self_attn.norm_k.weight"),
                               meta.rope_tab, grid, dx=dqkv[:, C:2 * C])
     acc("self_attn.norm_q.weight", dnq)

@@ -183,19 +183,24 @@ def ln_mod_bwd(dy, x, mean, rstd, dx, scale=None, w=None, accumulate=True):
     return colsum_reduce(p0), colsum_reduce(p1)
 
 
-def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None):
+# softmax_scale * log2(e) of head_dim 128: the out_scale that turns norm_q's output into the q
+# operand of the *_l2q attention entries (attn_fwd / attn_bwd with q_log2=True)
+L2Q_SCALE = 1.4426950408889634 / math.sqrt(128)
+
+
+def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None, out_scale=1.0):
     L, C = x.shape
     if out is None:
         out = torch.empty(L, C, dtype=BF16, device=x.device)
     rstd = torch.empty(L, dtype=torch.float32, device=x.device)
     f, h, ww = grid
     call("prfl_rms_rope_fwd", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps), ptr(rope_tab),
-         I64(f), I64(h), I64(ww), ptr(out), I64(_ld(out)), ptr(rstd), stream_ptr())
+         I64(f), I64(h), I64(ww), ptr(out), I64(_ld(out)), ptr(rstd), F32(out_scale), stream_ptr())
     return out, rstd
 
 
-def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None):
-    """returns (dx bf16, d w fp32)."""
+def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_scale=1.0):
+    """returns (dx bf16, d w fp32); out_scale as the forward's (dout is scaled by it)."""
     L, C = x.shape
     rp = call_int("prfl_norm_rows_per_part")
     p0 = torch.empty((L + rp - 1) // rp, C, dtype=torch.float32, device=x.device)
@@ -204,12 +209,14 @@ def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None):
     f, h, ww = grid
     call("prfl_rms_rope_bwd", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd), I64(L),
          I64(C), ptr(w), ptr(rope_tab), I64(f), I64(h), I64(ww), ptr(dx), I64(_ld(dx)), ptr(p0),
-         stream_ptr())
+         F32(out_scale), stream_ptr())
     return dx, colsum_reduce(p0)
 
 
-def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None):
-    """q [Lq, H*128], k/v [Lk, H*128] (row-strided views) -> (o bf16 [Lq, H*128], lse2 [H, Lq])."""
+def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None, q_log2=False):
+    """q [Lq, H*128], k/v [Lk, H*128] (row-strided views) -> (o bf16 [Lq, H*128], lse2 [H, Lq]).
+    q_log2: q is already multiplied by softmax_scale * log2(e) (rms_rope_fwd out_scale=L2Q_SCALE);
+    scale is then unused (prfl_attn_fwd_l2q_ws)."""
     Lq, C = q.shape
     Lk = k.shape[0]
     assert C == num_heads * 128, "head_dim must be 128"
@@ -221,13 +228,17 @@ def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None):
     # scratch for the split-KV tail of long-KV launches (0 bytes when the grid has no tail)
     nb = _lib.load().prfl_attn_fwd_ws_bytes(1, Lq, Lk, num_heads, k_len)
     ws = torch.empty(nb, dtype=torch.uint8, device=q.device) if nb > 0 else None
-    call("prfl_attn_fwd_ws", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
-         I64(_ld(v)), I64(0), ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk),
-         I64(num_heads), I64(k_len), F32(sc), ptr(ws), I64(nb), stream_ptr())
+    head = (ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v), I64(_ld(v)), I64(0),
+            ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk), I64(num_heads),
+            I64(k_len))
+    if q_log2:
+        call("prfl_attn_fwd_l2q_ws", *head, ptr(ws), I64(nb), stream_ptr())
+    else:
+        call("prfl_attn_fwd_ws", *head, F32(sc), ptr(ws), I64(nb), stream_ptr())
     return out, lse
 
 
-def attn_fwd_fp8(q, k, v, num_heads, k_len=None, out=None, scale=None):
+def attn_fwd_fp8(q, k, v, num_heads, k_len=None, out=None, scale=None, q_log2=False):
     """attn_fwd on the block-scaled e4m3 MFMA (config C5 self-attention): same arguments and
     outputs; q/k/v are quantised inside the call into a scratch buffer (~3 bytes per element)."""
     Lq, C = q.shape
@@ -240,13 +251,19 @@ def attn_fwd_fp8(q, k, v, num_heads, k_len=None, out=None, scale=None):
     lse = torch.empty(num_heads, Lq, dtype=torch.float32, device=q.device)
     nb = _lib.load().prfl_attn_fwd_fp8_ws_bytes(1, Lq, Lk, num_heads, k_len)
     ws = torch.empty(nb, dtype=torch.uint8, device=q.device)
-    call("prfl_attn_fwd_fp8", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
-         I64(_ld(v)), I64(0), ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq),
-         I64(Lk), I64(num_heads), I64(k_len), F32(sc), ptr(ws), I64(nb), stream_ptr())
+    head = (ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v), I64(_ld(v)), I64(0),
+            ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk), I64(num_heads),
+            I64(k_len))
+    if q_log2:
+        call("prfl_attn_fwd_fp8_l2q", *head, ptr(ws), I64(nb), stream_ptr())
+    else:
+        call("prfl_attn_fwd_fp8", *head, F32(sc), ptr(ws), I64(nb), stream_ptr())
     return out, lse
 
 
-def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=None, scale=None):
+def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=None, scale=None,
+             q_log2=False):
+    """Backward of attn_fwd; with q_log2 dq is the gradient w.r.t. the pre-scaled q."""
     Lq, C = q.shape
     Lk = k.shape[0]
     k_len = Lk if k_len is None else int(k_len)
@@ -259,11 +276,14 @@ def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=No
     # scratch for the split tails of long-KV launches (0 bytes when the grids have no tail)
     nb = _lib.load().prfl_attn_bwd_ws_bytes(1, Lq, Lk, num_heads, k_len)
     ws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb > 0 else None
-    call("prfl_attn_bwd_ws", ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v),
-         I64(_ld(v)), I64(0), ptr(o), I64(_ld(o)), I64(0), ptr(do), I64(_ld(do)), I64(0), ptr(lse),
-         ptr(delta), ptr(dq), I64(_ld(dq)), I64(0), ptr(dk), I64(_ld(dk)), I64(0), ptr(dv),
-         I64(_ld(dv)), I64(0), I64(1), I64(Lq), I64(Lk), I64(num_heads), I64(k_len), F32(sc),
-         ptr(ws), I64(nb), stream_ptr())
+    head = (ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v), I64(_ld(v)), I64(0),
+            ptr(o), I64(_ld(o)), I64(0), ptr(do), I64(_ld(do)), I64(0), ptr(lse), ptr(delta),
+            ptr(dq), I64(_ld(dq)), I64(0), ptr(dk), I64(_ld(dk)), I64(0), ptr(dv), I64(_ld(dv)),
+            I64(0), I64(1), I64(Lq), I64(Lk), I64(num_heads), I64(k_len))
+    if q_log2:
+        call("prfl_attn_bwd_l2q_ws", *head, ptr(ws), I64(nb), stream_ptr())
+    else:
+        call("prfl_attn_bwd_ws", *head, F32(sc), ptr(ws), I64(nb), stream_ptr())
     return dq, dk, dv
 
 

@@ -74,6 +74,14 @@ int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int6
                      int64_t k_len, float scale, void* ws, int64_t ws_bytes, void* stream);
 /* Scratch bytes prfl_attn_fwd_ws needs on the current device (0 = no split for this shape). */
 int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
+/* prfl_attn_fwd_ws with q in log2 units, q = q_orig * scale * log2(e) (the fused block's
+ * RMSNorm+RoPE writes it so, prfl_rms_rope_fwd out_scale): the S accumulators start at the running
+ * row max and P = exp2(S) takes one v_exp per score.  o / lse2 are those of
+ * prfl_attn_fwd_ws(q_orig, ..., scale); same scratch. */
+int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                         int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
+                         int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                         int64_t k_len, void* ws, int64_t ws_bytes, void* stream);
 /* Config C5 (fp8): the same forward on the block-scaled e4m3 MFMA.  q, k, v stay bf16 in the
  * layout above and are quantised inside the call (Q per token and head, K per head, V per head
  * and channel, V stored transposed) into the REQUIRED caller-owned scratch `ws` (256-B aligned)
@@ -85,6 +93,11 @@ int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k, int
                       int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
                       int64_t k_len, float scale, void* ws, int64_t ws_bytes, void* stream);
 int64_t prfl_attn_fwd_fp8_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
+/* prfl_attn_fwd_fp8 with q in log2 units (as prfl_attn_fwd_l2q_ws). */
+int prfl_attn_fwd_fp8_l2q(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                          int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
+                          int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                          int64_t k_len, void* ws, int64_t ws_bytes, void* stream);
 /* Backward of the above (flash-attn's _flash_attn_varlen_backward).  delta: [B][H][Lq] fp32
  * caller-owned workspace. */
 int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
@@ -107,6 +120,16 @@ int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int6
                      int64_t ws_bytes, void* stream);
 /* Scratch bytes prfl_attn_bwd_ws needs on the current device (0 = no split for this shape). */
 int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
+/* prfl_attn_bwd_ws for a q in log2 units (prfl_attn_fwd_l2q_ws): dq is the gradient w.r.t. that
+ * pre-scaled q (ln 2 * dS.K; the RMSNorm+RoPE backward's out_scale multiplies it back), dk / dv
+ * those of the unscaled problem; same scratch. */
+int prfl_attn_bwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                         int64_t bk, const void* v, int64_t ldv, int64_t bv, const void* o,
+                         int64_t ldo, int64_t bo, const void* dout, int64_t lddo, int64_t bdo,
+                         const float* lse2, float* delta, void* dq, int64_t lddq, int64_t bdq,
+                         void* dk, int64_t lddk, int64_t bdk, void* dv, int64_t lddv, int64_t bdv,
+                         int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len, void* ws,
+                         int64_t ws_bytes, void* stream);
 
 /* ---- single-query attention pooling (reward head) ----------------------------------------
  * Replaces the core of the 1-query nn.MultiheadAttention of QueryAttention
@@ -150,14 +173,16 @@ int prfl_norm_rows_per_part(void);
 /* WanRMSNorm (model.py:106-122) over all C channels + optional 3-D RoPE (rope_apply,
  * model.py:61-103; rope_tab = fp32 (cos,sin) [1024][64] of the complex freqs of model.py:521-526,
  * grid (F,Hg,Wg); rows >= F*Hg*Wg are not rotated; rope_tab == NULL -> no RoPE).
- *   out = bf16(rope(bf16(x * rsqrt(mean(x^2)+eps)) * w)) */
+ *   out = bf16(rope(bf16(x * rsqrt(mean(x^2)+eps)) * w) * out_scale)
+ * out_scale = 1 is the reference's norm_q / norm_k; softmax_scale * log2(e) yields the q operand of
+ * the *_l2q attention entries.  The backward scales the incoming gradient by out_scale. */
 int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w, float eps,
                       const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* out,
-                      int64_t ldo, float* rstd, void* stream);
+                      int64_t ldo, float* rstd, float out_scale, void* stream);
 int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
                       const float* rstd, int64_t L, int64_t C, const float* w,
                       const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                      int64_t lddx, float* part0, void* stream);
+                      int64_t lddx, float* part0, float out_scale, void* stream);
 
 /* ---- element-wise / reductions ------------------------------------------------------------ */
 /* autocast weight cast fp32 -> bf16 (the .to(bf16) of every Linear weight under autocast). */

@@ -198,6 +198,81 @@ def test_attention_fwd_bwd(ops, Lq, Lk, H, klen):
         assert dk[klen:].abs().max().item() == 0 and dv[klen:].abs().max().item() == 0
 
 
+SL2 = 1.4426950408889634 / math.sqrt(128)     # softmax_scale * log2(e), head_dim 128
+
+
+def _l2q(q):
+    """The *_l2q attention operand of a bf16 q: q2 = bf16(q * scale * log2 e) (what the fused
+    block's rms_rope_fwd writes), and the fp32 q that q2 represents exactly (q2 / (scale log2 e)),
+    the input of the reference computation."""
+    q2 = (q.float() * SL2).to(torch.bfloat16)
+    return q2, q2.float() / SL2
+
+
+@pytest.mark.parametrize("Lq,Lk,H,klen", [(200, 333, 2, 333), (105, 512, 2, 20),
+                                          (4200, 4200, 2, 4133), (4111, 5000, 1, 4500)])
+def test_attention_log2_q_vs_oracle(ops, Lq, Lk, H, klen):
+    """The q-in-log2-units entries (prfl_attn_fwd_l2q_ws / prfl_attn_bwd_l2q_ws: S accumulators
+    starting at the running max, one v_exp per score; the fused block's path) on the short-KV
+    (cross-attention) and long-KV (self-attention) instantiations vs the CPU oracle on the
+    q they represent; dq is the gradient w.r.t. the pre-scaled q (x scale log2 e = the oracle's)."""
+    g = torch.Generator().manual_seed(Lq * 7 + Lk)
+    C = H * 128
+    q2, qe = _l2q(bf(torch.randn(Lq, C, generator=g) * 1.5))
+    k = bf(torch.randn(Lk, C, generator=g) * 1.5)
+    v = bf(torch.randn(Lk, C, generator=g))
+    o, lse = ops.attn_fwd(q2.to(DEV), k.to(DEV), v.to(DEV), H, k_len=klen, q_log2=True)
+    qr = qe.view(1, Lq, H, 128).clone().requires_grad_(True)
+    kr = k.float().view(1, Lk, H, 128).requires_grad_(True)
+    vr = v.float().view(1, Lk, H, 128).requires_grad_(True)
+    ref = O.attention(qr, kr, vr, k_len=klen if klen < Lk else None)
+    assert rel(o, ref.reshape(Lq, C)) < 5e-3
+    lref = _lse2_ref(qe, k, H, klen, 1 / math.sqrt(128))
+    assert (lse.cpu() - lref).abs().max().item() < 1e-3
+    do = bf(torch.randn(Lq, C, generator=g))
+    ref.backward(do.float().view(1, Lq, H, 128))
+    dq, dk, dv = ops.attn_bwd(q2.to(DEV), k.to(DEV), v.to(DEV), o, do.to(DEV), lse, H, k_len=klen,
+                              q_log2=True)
+    assert rel(dq.float() * SL2, qr.grad.reshape(Lq, C)) < 2e-2
+    assert rel(dk, kr.grad.reshape(Lk, C)) < 2e-2
+    assert rel(dv, vr.grad.reshape(Lk, C)) < 2e-2
+    if klen < Lk:
+        assert dk[klen:].abs().max().item() == 0 and dv[klen:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("l2", [True, False])
+def test_attention_log2_q_extreme_rows(ops, l2):
+    """Rows whose scores all sit near -250 log2 units (exp2 of them underflows fp32) and rows with
+    scores in the hundreds plus one spike: the log2-q forward starts each row from its first
+    tile's max (the accumulators hold S - m), so neither underflows to an empty row nor
+    overflows; vs fp64 on the same bf16 operands."""
+    L, H = 4200, 1
+    C = H * 128
+    g = torch.Generator().manual_seed(3)
+    base = torch.randn(C, generator=g)
+    k = bf(base + 0.1 * torch.randn(L, C, generator=g))       # every key ~ base
+    v = bf(torch.randn(L, C, generator=g))
+    q = torch.randn(L, C, generator=g) * 0.05
+    bb = k.float().mean(0)
+    q[:64] += -bb / bb.norm() ** 2 * 250.0 / SL2               # scores ~ -250 +- a few
+    n = k[4000].float() - bb
+    q[64:128] += n / n.norm() ** 2 * 300.0 / SL2               # key 4000 stands out by ~300
+    q2 = (q * SL2).to(torch.bfloat16)
+    if l2:
+        o, lse = ops.attn_fwd(q2.to(DEV), k.to(DEV), v.to(DEV), H, q_log2=True)
+        s = q2[:128].double() @ k.double().t()                 # scores in log2 units
+    else:                                                      # the plain entry, same extremes
+        q1 = q.to(torch.bfloat16)
+        o, lse = ops.attn_fwd(q1.to(DEV), k.to(DEV), v.to(DEV), H)
+        s = q1[:128].double() @ k.double().t() * SL2
+    assert s[:64].max() < -200
+    exact = torch.softmax(s * math.log(2.0), -1) @ v.double()
+    assert torch.isfinite(o.float()).all() and torch.isfinite(lse).all()
+    assert rel(o[:128].cpu(), exact) < 5e-3
+    lref = torch.logsumexp(s * math.log(2.0), -1) / math.log(2.0)
+    assert (lse[0, :128].cpu().double() - lref).abs().max().item() < 1e-2
+
+
 def _lse2_ref(q, k, H, klen, scale):
     """log2-domain row LSE of softmax(q k^T * scale) over keys < klen; q/k bf16 [L, H*128]."""
     Lq, Lk = q.shape[0], k.shape[0]
@@ -273,8 +348,8 @@ def _attention_ref_gpu(q, k, v, do, H, scale, chunk=4096):
     return o, lse2, dq, dk, dv
 
 
-@pytest.mark.parametrize("L,H", [(32760, 2), (73920, 1)])
-def test_attention_full_size_vs_reference(ops, L, H):
+@pytest.mark.parametrize("L,H,l2", [(32760, 2, False), (73920, 1, False), (73920, 1, True)])
+def test_attention_full_size_vs_reference(ops, L, H, l2):
     """Self-attention at the real token counts (480p x 81f: L = 32 760, L % 96 = 24, L % 256 =
     248; 720p x 81f: L = 73 920) against an fp32 GPU restatement of the FA2 numerics; the
     forward rows are also checked against an fp64 CPU computation over all keys."""
@@ -285,8 +360,14 @@ def test_attention_full_size_vs_reference(ops, L, H):
     v = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
     do = torch.randn(L, C, generator=g, device=DEV).to(torch.bfloat16)
     scale = 1 / math.sqrt(128)
-    o, lse = ops.attn_fwd(q, k, v, H)
-    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, H)
+    if l2:       # the fused block's path: q in log2 units; references on the q it represents
+        q2, q = _l2q(q)
+        o, lse = ops.attn_fwd(q2, k, v, H, q_log2=True)
+        dq, dk, dv = ops.attn_bwd(q2, k, v, o, do, lse, H, q_log2=True)
+        dq = dq.float() * SL2
+    else:
+        o, lse = ops.attn_fwd(q, k, v, H)
+        dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, H)
     ro, rlse, rdq, rdk, rdv = _attention_ref_gpu(q, k, v, do, H, scale)
     assert rel(o, ro) < 5e-3
     assert (lse - rlse).abs().max().item() < 1e-3
@@ -410,7 +491,10 @@ def test_ln_mod(ops, C, x_bf16, affine):
 
 
 @pytest.mark.parametrize("rope", [True, False])
-def test_rms_rope(ops, rope):
+@pytest.mark.parametrize("osc", [1.0, 1.4426950408889634 / math.sqrt(128)])
+def test_rms_rope(ops, rope, osc):
+    """RMSNorm (+ RoPE) vs the oracle; osc = the out_scale that writes q in log2 units for the
+    *_l2q attention entries (the backward scales the incoming gradient by it)."""
     C, H = 256, 2
     grid = (3, 5, 7)
     L = 112   # 105 rotated + 7 pass-through rows
@@ -419,17 +503,19 @@ def test_rms_rope(ops, rope):
     w = 1 + torch.randn(C, generator=g) * 0.1
     freqs = O.rope_freqs(128)
     tab = ops.rope_table(freqs, DEV) if rope else None
-    out, rstd = ops.rms_rope_fwd(x.to(DEV), w.to(DEV), 1e-6, tab, grid if rope else (0, 0, 0))
+    out, rstd = ops.rms_rope_fwd(x.to(DEV), w.to(DEV), 1e-6, tab, grid if rope else (0, 0, 0),
+                                 out_scale=osc)
     xr = x.float().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     n = O.rms_norm(xr, wr)
     if rope:
         n = O.rope_apply(n.view(1, L, H, 128), torch.tensor([grid]), freqs).view(L, C)
+    n = n * osc
     assert rel(out, O.bf(n)) < 3e-3
     do = bf(torch.randn(L, C, generator=g))
     n.backward(do.float())
     dx, dw = ops.rms_rope_bwd(do.to(DEV), x.to(DEV), rstd, w.to(DEV), tab,
-                              grid if rope else (0, 0, 0))
+                              grid if rope else (0, 0, 0), out_scale=osc)
     assert rel(dx, xr.grad) < 1e-2
     assert rel(dw, wr.grad) < 5e-3
 

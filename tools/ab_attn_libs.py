@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--bwd", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="time prfl_attn_fwd_fp8 (config C5) instead")
+    ap.add_argument("--qs", default="", help="comma list of lib indices built with ATTN_QS=1: they "
+                    "get q pre-scaled by softmax_scale * log2(e) (rounded to bf16 once)")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     L, H, C = a.L, 40, 5120
@@ -31,9 +33,12 @@ def main():
                  dv=torch.empty(L, C, dtype=torch.bfloat16, device=dev)) for _ in libs]
     sc = 128 ** -0.5
     st = torch.cuda.current_stream().cuda_stream
+    qs_libs = {int(i) for i in a.qs.split(",") if i}
+    qsc = qkv[:, :C].float().mul(sc * 1.4426950408889634).to(torch.bfloat16).contiguous()
 
     def fwd(lib, b):
-        args = (q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+        qq = (qsc.data_ptr(), C, 0) if b.get("qs") else (q.data_ptr(), 3 * C, 0)
+        args = (*qq, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
                 b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc)
         if a.fp8:
             nb = lib.prfl_attn_fwd_fp8_ws_bytes(1, L, L, H, L)
@@ -49,10 +54,13 @@ def main():
             assert lib.prfl_attn_fwd(*args, st) == 0
 
     def bwd(lib, b):
-        args = (q.data_ptr(), 3 * C, 0, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
+        # ATTN_BWD_QS builds: q pre-scaled, gradient scale ln 2 (dK = ln2 * dS^T q')
+        qq = (qsc.data_ptr(), C, 0) if b.get("qs") else (q.data_ptr(), 3 * C, 0)
+        gsc = 0.6931471805599453 if b.get("qs") else sc
+        args = (*qq, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
                 b["o"].data_ptr(), C, 0, do.data_ptr(), C, 0, b["lse"].data_ptr(),
                 b["delta"].data_ptr(), b["dq"].data_ptr(), C, 0, b["dk"].data_ptr(), C, 0,
-                b["dv"].data_ptr(), C, 0, 1, L, L, H, L, sc)
+                b["dv"].data_ptr(), C, 0, 1, L, L, H, L, gsc)
         if lib.has_bws:
             nb = lib.prfl_attn_bwd_ws_bytes(1, L, L, H, L)
             if "bws" not in b or b["bws"].numel() < nb:
@@ -61,6 +69,8 @@ def main():
         else:
             assert lib.prfl_attn_bwd(*args, st) == 0
 
+    for i in qs_libs:
+        outs[i]["qs"] = True
     work = [("fwd", fwd, 4 * L * L * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
     for w, fn, fl in work:
         ts = [[] for _ in libs]
