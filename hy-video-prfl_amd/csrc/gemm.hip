@@ -296,9 +296,6 @@ constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
 constexpr int TILE2 = BM2 * BK * 2;                    // 32 KiB per operand per stage
 
 
-#ifndef GEMM_M0_GROUP
-#define GEMM_M0_GROUP 0
-#endif
 #ifndef GEMM_GROUP_M
 #define GEMM_GROUP_M 4        // 256-row blocks walked together per XCD (L2 / MALL reuse of B)
 #endif
@@ -680,32 +677,33 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
                            : make_srd(g.A + m0, (uint32_t)((int64_t)g.K * g.lda * 2 - (int64_t)m0 * 2));
   const i32x4 srd_b = B_KC ? make_srd(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(g.N - n0) * g.ldb * 2))
                            : make_srd(g.B + n0, (uint32_t)((int64_t)g.K * g.ldb * 2 - (int64_t)n0 * 2));
+  // DMA pieces: the wave's 4 pieces of an operand are consecutive KiB of LDS, so one m0 (the
+  // first piece's LDS address) serves all four, piece i adding i KiB through the instruction
+  // offset; that offset also adds to the global address, so it is pre-subtracted from the per-lane
+  // offsets (never below zero: K-major ld >= K >= 128, MN-major ld >= 256 under fits256).
+  // One m0 write per 4 pieces instead of a save / set / nop / restore per piece: dX +3-7 %,
+  // forward +0.2-2.8 %, bit-identical (profiles/r03_gemm_m0group_ab.txt)
   uint32_t offa[4], offb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i);
-    offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i);
+    offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i) - i * 1024;
+    offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i) - i * 1024;
   }
-#if GEMM_M0_GROUP
   unsigned m0keep = 0;
-  uint32_t offa_main[4], offb_main[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {       // prologue keeps the per-piece form; the loop's grouped form
-    offa_main[i] = offa[i] - i * 1024;   // adds i KiB back through the instruction offset
-    offb_main[i] = offb[i] - i * 1024;
-  }
-#endif
   // k0 -> soffset: 2 B per k for K-major operands, one row (ld elements) per k for MN-major
   auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
   auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
+  // piece i (< 8: A pieces 0-3, B pieces 4-7) of slice j into ring slot sd
+  auto piece = [&](int i, int j, char* sd) {
+    if (i == 0 || i == 4) m0_set(lds_addr(sd + (i ? HALF4 : 0) + wid * 4096), m0keep);
+    if (i < 4) dma16_buf_m0(srd_a, offa[i], soff_a(j), i);
+    else dma16_buf_m0(srd_b, offb[i - 4], soff_b(j), i - 4);
+    if (i == 3 || i == 7) m0_restore(m0keep);
+  };
   auto issue = [&](int j) {
     j = min(j, ns - 1);
-    char* st = smem + (j & 3) * SLICE4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16_buf(srd_a, offa[i], soff_a(j), lds_addr(st + (wid * 4 + i) * 1024));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dma16_buf(srd_b, offb[i], soff_b(j), lds_addr(st + HALF4 + (wid * 4 + i) * 1024));
+    for (int i = 0; i < 8; ++i) piece(i, j, smem + (j & 3) * SLICE4);
   };
   auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
     const char* st = smem + (j & 3) * SLICE4;
@@ -726,18 +724,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-#if GEMM_M0_GROUP
-      // one m0 per operand: the wave's 4 pieces are consecutive KiB of LDS, piece i at the
-      // instruction offset i KiB (its global offset was pre-compensated in offa / offb)
-      if (i == 0 || i == 4)
-        m0_set(lds_addr(sd + (i ? HALF4 : 0) + wid * 4096), m0keep);
-      if (i < 4) dma16_buf_m0(srd_a, offa_main[i], soff_a(jd), i);
-      else dma16_buf_m0(srd_b, offb_main[i - 4], soff_b(jd), i - 4);
-      if (i == 3 || i == 7) m0_restore(m0keep);
-#else
-      if (i < 4) dma16_buf(srd_a, offa[i], soff_a(jd), lds_addr(sd + (wid * 4 + i) * 1024));
-      else dma16_buf(srd_b, offb[i - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + i - 4) * 1024));
-#endif
+      piece(i, jd, sd);
       na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
       nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
 #pragma unroll
@@ -933,22 +920,26 @@ __global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
                            : make_srd(g.A + m0, (uint32_t)((int64_t)g.K * g.lda * 2 - (int64_t)m0 * 2));
   const i32x4 srd_b = B_KC ? make_srd(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(g.N - n0) * g.ldb * 2))
                            : make_srd(g.B + n0, (uint32_t)((int64_t)g.K * g.ldb * 2 - (int64_t)n0 * 2));
+  // grouped DMA pieces (one m0 per operand, piece i at instruction offset i KiB), as gemm4w_kernel
   uint32_t offa[4], offb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    offa[i] = piece_off32<A_KC>(g.lda, wid, lane, i);
-    offb[i] = piece_off32<B_KC>(g.ldb, wid, lane, i);
+    offa[i] = piece_off32<A_KC>(g.lda, wid, lane, i) - i * 1024;
+    offb[i] = piece_off32<B_KC>(g.ldb, wid, lane, i) - i * 1024;
   }
+  unsigned m0keep = 0;
   auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
   auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
+  auto piece = [&](int i, int j, char* sd) {
+    if (i == 0 || i == 4) m0_set(lds_addr(sd + (i ? HALF4 : 0) + wid * 4096), m0keep);
+    if (i < 4) dma16_buf_m0(srd_a, offa[i], soff_a(j), i);
+    else dma16_buf_m0(srd_b, offb[i - 4], soff_b(j), i - 4);
+    if (i == 3 || i == 7) m0_restore(m0keep);
+  };
   auto issue = [&](int j) {
     j = min(j, ns - 1);
-    char* st = smem + (j & 3) * SLICE4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16_buf(srd_a, offa[i], soff_a(j), lds_addr(st + (wid * 4 + i) * 1024));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dma16_buf(srd_b, offb[i], soff_b(j), lds_addr(st + HALF4 + (wid * 4 + i) * 1024));
+    for (int i = 0; i < 8; ++i) piece(i, j, smem + (j & 3) * SLICE4);
   };
   // fragment c = 4 s + i: k-step s, 32-row block i of the wave's 128 rows (A) / columns (B)
   auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
@@ -969,8 +960,7 @@ __global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
     // slice j+3 and the reads of fragments c of slice j+1
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      if (c < 4) dma16_buf(srd_a, offa[c], soff_a(jd), lds_addr(sd + (wid * 4 + c) * 1024));
-      else dma16_buf(srd_b, offb[c - 4], soff_b(jd), lds_addr(sd + HALF4 + (wid * 4 + c - 4) * 1024));
+      piece(c, jd, sd);
       na[c] = read_frag32<A_KC>(st, wm * 128 + (c & 3) * 32, c >> 2, lane);
       nb[c] = read_frag32<B_KC>(st + HALF4, wn * 128 + (c & 3) * 32, c >> 2, lane);
       const int s = c >> 2, i = c & 3;

@@ -29,6 +29,12 @@ def load(path):
         lib.prfl_attn_fwd_fp8.argtypes, lib.prfl_attn_fwd_fp8.restype = FWD[:-1] + [P, I64, P], ctypes.c_int
         lib.prfl_attn_fwd_fp8_ws_bytes.argtypes = [I64] * 5
         lib.prfl_attn_fwd_fp8_ws_bytes.restype = I64
+    lib.has_l2q = hasattr(lib, "prfl_attn_fwd_l2q_ws")
+    if lib.has_l2q:   # q in log2 units (the fused block's path): no scale argument
+        lib.prfl_attn_fwd_l2q_ws.argtypes = FWD[:-2] + [P, I64, P]
+        lib.prfl_attn_fwd_l2q_ws.restype = ctypes.c_int
+        lib.prfl_attn_bwd_l2q_ws.argtypes = BWD[:-2] + [P, I64, P]
+        lib.prfl_attn_bwd_l2q_ws.restype = ctypes.c_int
     lib.has_bws = hasattr(lib, "prfl_attn_bwd_ws")
     if lib.has_bws:
         lib.prfl_attn_bwd_ws.argtypes, lib.prfl_attn_bwd_ws.restype = BWD[:-1] + [P, I64, P], ctypes.c_int

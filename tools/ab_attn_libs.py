@@ -49,7 +49,10 @@ def main():
             nb = lib.prfl_attn_fwd_ws_bytes(1, L, L, H, L)
             if "ws" not in b or b["ws"].numel() < nb:
                 b["ws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
-            assert lib.prfl_attn_fwd_ws(*args, b["ws"].data_ptr(), nb, st) == 0
+            if b.get("qs") and lib.has_l2q:
+                assert lib.prfl_attn_fwd_l2q_ws(*args[:-1], b["ws"].data_ptr(), nb, st) == 0
+            else:
+                assert lib.prfl_attn_fwd_ws(*args, b["ws"].data_ptr(), nb, st) == 0
         else:
             assert lib.prfl_attn_fwd(*args, st) == 0
 
@@ -65,7 +68,10 @@ def main():
             nb = lib.prfl_attn_bwd_ws_bytes(1, L, L, H, L)
             if "bws" not in b or b["bws"].numel() < nb:
                 b["bws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
-            assert lib.prfl_attn_bwd_ws(*args, b["bws"].data_ptr(), nb, st) == 0
+            if b.get("qs") and lib.has_l2q:
+                assert lib.prfl_attn_bwd_l2q_ws(*args[:-1], b["bws"].data_ptr(), nb, st) == 0
+            else:
+                assert lib.prfl_attn_bwd_ws(*args, b["bws"].data_ptr(), nb, st) == 0
         else:
             assert lib.prfl_attn_bwd(*args, st) == 0
 
