@@ -26,24 +26,32 @@ if which == "attn_fp8":
         torch.cuda.synchronize()
         dt = time.time() - t0
         print(f"attn_fp8 {dt*1e3:.2f} ms  {fl/dt/1e12:.0f} TF/s", flush=True)
-elif which in ("attn", "attn_bwd"):
+elif which in ("attn", "attn_bwd", "attn_l2q", "attn_bwd_l2q"):
+    # *_l2q: the fused block's path (q in log2 units, prfl_attn_*_l2q entries)
+    l2 = which.endswith("_l2q")
+    which = which.replace("_l2q", "")
     qkv = torch.randn(L, 3 * C, device=dev, generator=g).to(torch.bfloat16)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-    o, lse = ops.attn_fwd(q, k, v, NH)
+    if l2:
+        q = (q.float() * ops.L2Q_SCALE).to(torch.bfloat16)
+    o, lse = ops.attn_fwd(q, k, v, NH, q_log2=l2)
     do = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
     fl = 4 * L * L * C
     for i in range(reps):
         torch.cuda.synchronize()
         t0 = time.time()
         if which == "attn":
-            ops.attn_fwd(q, k, v, NH, out=o)
+            ops.attn_fwd(q, k, v, NH, out=o, q_log2=l2)
         else:
-            ops.attn_bwd(q, k, v, o, do, lse, NH)
+            ops.attn_bwd(q, k, v, o, do, lse, NH, q_log2=l2)
         torch.cuda.synchronize()
         dt = time.time() - t0
         print(f"{which} {dt*1e3:.2f} ms  {fl*(1 if which=='attn' else 2.5)/dt/1e12:.0f} TF/s", flush=True)
     ops.prof_enable(True)
-    ops.attn_fwd(q, k, v, NH, out=o) if which == "attn" else ops.attn_bwd(q, k, v, o, do, lse, NH)
+    if which == "attn":
+        ops.attn_fwd(q, k, v, NH, out=o, q_log2=l2)
+    else:
+        ops.attn_bwd(q, k, v, o, do, lse, NH, q_log2=l2)
     torch.cuda.synchronize()
     ops.prof_enable(False)
     for kname, d in ops.prof_collect().items():
