@@ -390,7 +390,11 @@ def main():
         steps, durs = 0, []
         for i in range(args.steps):
             one(9 + 5 * i)                   # every timed iteration ends on an optimizer step
-            torch.cuda.synchronize()
+            # main stream only: the reward step's optimizer update (moments streamed over PCIe
+            # on the optimizer's side streams) runs on under the next iteration's first forward,
+            # each block waiting for its own parameters (optim.py attach), as in a training loop;
+            # the synchronize after the loop puts the last update inside the timed window
+            torch.cuda.current_stream().synchronize()
             steps += 1
             t_it = time.time() - t0 - sum(durs)
             durs.append(t_it)

@@ -177,9 +177,6 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_LAZY_TAU
 #define ATTN_LAZY_TAU 8
 #endif
-#ifndef ATTN_PV_FIRST
-#define ATTN_PV_FIRST 0
-#endif
 // q-in-log2 forward (QS): P = exp2(S') first and the max pass only when the tile sum says some
 // P exceeded 2^TAU (S' recomputed from the still-staged K tile), instead of a max pass over every
 // tile: 720p forward 89.94 -> 88.28 ms, bit-identical while no rescale triggers
@@ -305,51 +302,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
     if (!ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-#if ATTN_PV_FIRST
-    if (t > 0) {
-      const char* Vs = smem + stp * SB;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int ro = (kt * 32 + 16 * s2) * 256;
-            const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
-            o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
-          }
-      }
-      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
-#pragma unroll
-        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);   // P(t-1) dies before S(t) is born
-    if (t < nkv) {
-      const char* Ks = smem + st * SB;
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-        s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], QS ? negm : (f32x16){});
-#pragma unroll
-        for (int ks = 1; ks < 8; ++ks)
-          s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
-      }
-      if (SCHED) {   // K-row reads SCHED+1 MFMAs ahead, one per MFMA gap
-        __builtin_amdgcn_sched_group_barrier(0x100, SCHED + 1, 0);
-#pragma unroll
-        for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
-      }
-    }
-#else
     if (t < nkv) {
       const char* Ks = smem + st * SB;
 #pragma unroll
@@ -392,7 +344,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
-#endif
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     // ---------------- Y_t ----------------

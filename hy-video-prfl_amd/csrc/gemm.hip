@@ -596,56 +596,75 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 #pragma unroll
     for (int i = 0; i < EPI4_AHEAD; ++i) load_in(i, buf[i]);
   }
+  // bf16 outputs of fragments j, j+1 leave as ONE 16-B store per lane (MI355X guide T21, with
+  // v_permlane16_swap: lane group g holds columns 4g..4g+3 of a 16-column fragment; swapping
+  // groups 1 <-> 0 and 3 <-> 2 between the two fragments gives every lane 8 contiguous columns,
+  // at column offset 16 (g & 1) + 8 (g >> 1) of the pair) when the wave's 128 columns are in
+  // range and the rows 16-B aligned; else the two 8-B stores as computed
+  const int gq = (threadIdx.x & 63) >> 4, nw = nb - 4 * gq;
+  const int woff = 16 * (gq & 1) + 8 * (gq >> 1);
+  const bool cols_in = nw + 128 <= g.N;
+  const bool wide_c = cols_in && (g.ldc % 8) == 0 && (((uintptr_t)g.C) & 15) == 0;
+  const bool wide_x = cols_in && (g.ldaux % 8) == 0 && (((uintptr_t)g.aux) & 15) == 0;
+  auto st_pair = [&](bf16* base, int64_t ld, bool wide, int m, int j, bf16x4 a, bf16x4 b) {
+    bf16* row = base + (int64_t)m * ld;
+    if (wide) {
+      const u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+      const auto r0 = __builtin_amdgcn_permlane16_swap(ua[0], ub[0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(ua[1], ub[1], false, false);
+      *(u32x4*)(row + nw + 16 * j + woff) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+    } else {
+      if (nb + 16 * j < g.N) *(bf16x4*)(row + nb + 16 * j) = a;
+      if (nb + 16 * j + 16 < g.N) *(bf16x4*)(row + nb + 16 * j + 16) = b;
+    }
+  };
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (HAS_IN && i + EPI4_AHEAD < 8) load_in(i + EPI4_AHEAD, buf[i + EPI4_AHEAD]);
     const int m = mb + 16 * i;
     if (m < g.M) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int n = nb + 16 * j;
-        if (n >= g.N) continue;
-        const f32x4 v = acc[i][j];
-        if (EPI == EPI_F32) {
-          *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + widen(buf[i][j]) : v;
-        } else if (EPI == EPI_DGELU) {
-          const f32x4 pre = widen(buf[i][j]);
-          bf16x4 o;
+      for (int j = 0; j < 8; j += 2) {
+        bf16x4 oc[2], ox[2];          // bf16 results for C / aux of fragments j, j + 1
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
-          *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-        } else {
-          float y[4];
+        for (int h = 0; h < 2; ++h) {
+          const int jj = j + h, n = nb + 16 * jj;
+          const f32x4 v = acc[i][jj];
+          if (EPI == EPI_F32) {
+            if (n < g.N)
+              *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + widen(buf[i][jj]) : v;
+          } else if (EPI == EPI_DGELU) {
+            const f32x4 pre = widen(buf[i][jj]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bias[j][r]);
-          if (EPI == EPI_BF16) {
-            bf16x4 o;
+            for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
+          } else {
+            float y[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(y[r]);
-            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-          } else if (EPI == EPI_GELU) {
-            bf16x4 o, pre;
+            for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bias[jj][r]);
+            if (EPI == EPI_BF16) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              pre[r] = f2bf(y[r]);
-              o[r] = f2bf(gelu_tanh(y[r]));
+              for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(y[r]);
+            } else if (EPI == EPI_GELU) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ox[h][r] = f2bf(y[r]);
+                oc[h][r] = f2bf(gelu_tanh(y[r]));
+              }
+            } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) ox[h][r] = f2bf(y[r]);
+              const f32x4 res = widen(buf[i][jj]);
+              f32x4 o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gate[jj][r]);
+              if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
             }
-            if (g.aux) *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = pre;
-            *(bf16x4*)((bf16*)g.C + (int64_t)m * g.ldc + n) = o;
-          } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
-            if (g.aux) {
-              bf16x4 yo;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) yo[r] = f2bf(y[r]);
-              *(bf16x4*)(g.aux + (int64_t)m * g.ldaux + n) = yo;
-            }
-            const f32x4 res = widen(buf[i][j]);
-            f32x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gate[j][r]);
-            *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
           }
         }
+        if (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)
+          st_pair((bf16*)g.C, g.ldc, wide_c, m, j, oc[0], oc[1]);
+        if ((EPI == EPI_GELU || EPI == EPI_RESID) && g.aux)
+          st_pair(g.aux, g.ldaux, wide_x, m, j, ox[0], ox[1]);
       }
     }
   }

@@ -4,7 +4,14 @@ Merges every kernel's [start, end] interval (all queues) and reports, over the t
 given window, seconds from the first kernel), busy time, idle time, the largest idle gaps and the
 kernels that precede them (what the GPU waited on the host after)."""
 import csv
+import re
 import sys
+
+
+def short(n):
+    n = re.sub(r"^void ", "", n)
+    n = re.sub(r"\(anonymous namespace\)::", "", n)
+    return re.split(r"[<(]", n)[0][:48]
 
 
 def main():
@@ -36,12 +43,17 @@ def main():
     print(f"gaps > 0.1 ms: {len(big)} totalling {sum(g[0] for g in big) / 1e9:.2f} s")
     by = {}
     for g, p, n, _ in gaps:
-        k = p.split("(")[0][:60]
+        k = short(p)
         by[k] = by.get(k, 0) + g
+    hist = [0, 0, 0, 0, 0]
+    for g, _, _, _ in gaps:
+        hist[min(4, sum(g > t for t in (1e4, 1e5, 1e6, 1e7)))] += g
+    print("idle by gap size  <10us %.2f s | 10-100us %.2f s | 0.1-1ms %.2f s | 1-10ms %.2f s | "
+          ">10ms %.2f s" % tuple(h / 1e9 for h in hist))
     for k, v in sorted(by.items(), key=lambda kv: -kv[1])[:12]:
         print(f"  idle after {k:60s} {v / 1e9:8.3f} s")
     for g, p, n, at in sorted(gaps, reverse=True)[:15]:
-        print(f"  {g / 1e6:9.2f} ms at {at / 1e9:8.2f} s after {p.split('(')[0][:50]} -> {n.split('(')[0][:50]}")
+        print(f"  {g / 1e6:9.2f} ms at {at / 1e9:8.2f} s after {short(p)} -> {short(n)}")
 
 
 if __name__ == "__main__":
