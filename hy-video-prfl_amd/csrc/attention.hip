@@ -761,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
 // LSE and D are per-lane scalars), dS^T = P^T (dP^T - D) packed to bf16, dQ^T += K^T dS^T.  The
 // K / V tiles arrive by LDS-DMA into a 2-stage ring (tile t+1 issued at the top of tile t,
 // retired by vmcnt(0) + the one barrier per tile).
-template <int NKT>
+template <int NKT, bool QS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
   __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
@@ -787,6 +787,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
   const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
   const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
+  // QS (q in log2 units): -Q fragments and S accumulators starting at this query's LSE give
+  // LSE - S' = -(S' - LSE), so P = exp2 of its negation (the v_exp neg modifier): no FMA per
+  // score; the tuple costs 16 VGPRs, paid for by packing dS one key sub-tile at a time
+  f32x16 lset;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lset[r] = lse;
+  if (QS) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = -qf[ks];
+  }
   f32x16 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -835,21 +845,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     if (!ATTN_BWD_DMA_MID && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
     const char* Ks = smem + (t & 1) * SB;
     const char* Vs = Ks + SV;
-    bf16x8 dsp[NKT][2];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       f32x16 st, dpt;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
       const int row = kt * 32 + l32;
+      st = mfma32(*(const bf16x8*)(Ks + offB(row, hh * 16)), qf[0], QS ? lset : st);
+      dpt = mfma32(*(const bf16x8*)(Vs + off16(row, hh)), df[0], dpt);
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
+      for (int ks = 1; ks < 8; ++ks) {
         st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
         dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
+        const float p = QS ? __builtin_amdgcn_exp2f(-st[r]) : __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
         dpt[r] = ATTN_BWD_NEGD ? p * (dpt[r] + del) : p * (dpt[r] - del);   // del = -D there
       }
       if (__builtin_expect(kb + kt * 32 + 32 > a.k_len, 0)) {   // keys >= k_len: dS = 0
@@ -857,24 +868,24 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         for (int r = 0; r < 16; ++r)
           if (kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) dpt[r] = 0.f;
       }
+      bf16x8 dsp[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
-        dsp[kt][s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                               f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                               f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+        dsp[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                           f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                           f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
       if (ATTN_BWD_DMA_MID && kt == 0 && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
-    }
+      // dQ^T += K^T dS^T for this key sub-tile (per dQ tile the same (kt, s2) summation order)
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt)
+      for (int dt = 0; dt < 4; ++dt) {
+        const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
           const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
-          dq[dt] = mfma32(kf, dsp[kt][s2], dq[dt]);
+          dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
         }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1729,7 +1740,10 @@ int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();
   prfl_prof::begin(KID_ATTN_BWD_DQ, s);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
+  if (l2q)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
   if (rq) hipLaunchKernelGGL(attn_merge_q_kernel, dim3((unsigned)rq, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(6.0 * B * H * HD * (double)Lq * (double)k_len);
   prfl_prof::end(KID_ATTN_BWD_DQ, s);
