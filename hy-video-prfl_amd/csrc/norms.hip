@@ -321,74 +321,6 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
   }
 }
 
-// RMSNorm + RoPE forward, one wave per row (RPW rows per wave, w staged in LDS once per
-// workgroup): the wave reduction replaces the block reduction and its two barriers per row, and a
-// lane's chunks c = lane + 64 j all sit at element (4 lane) mod 128 of their head, so its two
-// complex pairs -- and their (cos, sin) -- are the same in every chunk: 2 table loads per row and
-// lane instead of 2 per chunk.  Same arithmetic per element as rms_rope_fwd_kernel; the sum of
-// squares is reduced in another order (rstd within an ulp).
-__global__ __launch_bounds__(NT) void rms_rope_fwd_w_kernel(
-    const bf16* __restrict__ x, int64_t ldx, int L, int C, const float* __restrict__ w, float eps,
-    const float2* __restrict__ tab, int F, int Hg, int Wg, bf16* __restrict__ out, int64_t ldo,
-    float* __restrict__ rstd_out, float oscale) {
-  __shared__ f32x4 wl[WV * 64];
-  const int nc = C / 4;
-  for (int c = threadIdx.x; c < nc; c += NT) wl[c] = ldf4(w, c * 4);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int p0 = ((4 * lane) & 127) >> 1;      // the lane's first complex pair within a head
-  const int64_t row0 = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RPW;
-  for (int rr = 0; rr < RPW; ++rr) {
-    const int64_t row = row0 + rr;
-    if (row >= L) return;
-    f32x4 v[WV];
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < WV; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        v[j] = ld4(x, row * ldx + c * 4, 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ss += v[j][r] * v[j][r];
-      }
-    }
-    const float rstd = rsqrtf(wave_sum(ss) / C + eps);
-    int pf, ph, pw;
-    bool rot;
-    rope_pos(row, F, Hg, Wg, pf, ph, pw, rot);
-    rot = rot && tab != nullptr;
-    float2 cs[2] = {{1.f, 0.f}, {1.f, 0.f}};
-    if (rot) {
-      cs[0] = tab[rope_index(p0, pf, ph, pw) * 64 + p0];
-      cs[1] = tab[rope_index(p0 + 1, pf, ph, pw) * 64 + p0 + 1];
-    }
-#pragma unroll
-    for (int j = 0; j < WV; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        const f32x4 wv = wl[c];
-        float y[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = mul_rn(bfr(v[j][r] * rstd), wv[r]);
-        bf16x4 o;
-        if (rot) {
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            const float a = y[2 * pp], bq = y[2 * pp + 1];
-            o[2 * pp] = f2bf(__fmul_rn(__fsub_rn(__fmul_rn(a, cs[pp].x), __fmul_rn(bq, cs[pp].y)), oscale));
-            o[2 * pp + 1] = f2bf(__fmul_rn(__fadd_rn(__fmul_rn(a, cs[pp].y), __fmul_rn(bq, cs[pp].x)), oscale));
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bf(__fmul_rn(y[r], oscale));
-        }
-        *(bf16x4*)(out + row * ldo + c * 4) = o;
-      }
-    }
-    if (lane == 0) rstd_out[row] = rstd;
-  }
-}
-
 constexpr int BWD_ROWS = 32;
 bool bad_c(int64_t C) { return C <= 0 || (C % 4) != 0 || C > 4 * MAXV * NT; }
 }  // namespace
@@ -438,15 +370,11 @@ extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t 
   if (bad_c(C)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
-  if (C % 128 == 0 && C <= 4 * WV * 64)   // whole heads: every chunk of a lane at one head offset
-    hipLaunchKernelGGL(rms_rope_fwd_w_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
-                       dim3(NT), 0, s, (const bf16*)x, ldx, (int)L, (int)C, w, eps,
-                       (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd,
-                       out_scale);
-  else
-    hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C, w,
-                       eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd,
-                       out_scale);
+  // (a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p:
+  // profiles/r03_ab_rms_rope_wave.txt)
+  hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C, w,
+                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd,
+                     out_scale);
   prfl_prof::set_work((double)L * C * 4);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();
