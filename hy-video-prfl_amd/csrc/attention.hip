@@ -181,9 +181,6 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // P exceeded 2^TAU (S' recomputed from the still-staged K tile), instead of a max pass over every
 // tile: 720p forward 89.94 -> 88.28 ms, bit-identical while no rescale triggers
 // (profiles/r03_ab_attn_sumcheck.txt); 0 = max pass every tile
-#ifndef ATTN_DMA_G1
-#define ATTN_DMA_G1 0
-#endif
 #ifndef ATTN_SUMCHECK
 #define ATTN_SUMCHECK 1
 #endif
@@ -284,26 +281,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
       dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
-  // ATTN_DMA_G1: waves 4-7 issue the WHOLE tile t+2 in Y_t (6 K + 6 V pieces each, per-lane
-  // offsets re-derived from a volatile lane id: no registers kept live), waves 0-3 none; every
-  // piece then has two phases to land (retired by the vmcnt(0) that ends waves 4-7's X_{t+1})
-  auto dma_all = [&](int t, int st) {
-    char* Ks = smem + st * SB;
-    char* Vs = Ks + SV;
-    const int tg = t0 + t;
-    const int rows = min(a.Lk - tg * TK, TK);
-    const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
-    const i32x4 sv = make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
-    uint32_t ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-#pragma unroll
-    for (int i = 0; i < 2 * NKT; ++i) {
-      const int pc = (w - 4) * 2 * NKT + i, row = pc * 4 + (ln >> 4), c = ln & 15;
-      const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16_buf(sk, (uint32_t)(row * a.ldk * 2) + ((c ^ (row & 15)) << 4), 0, lds_addr(Ks + pc * 1024));
-      dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((c ^ swzb) << 4), 0, lds_addr(Vs + pc * 1024));
-    }
-  };
   auto bar = [&]() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -324,7 +301,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   int st = 0, stp = 2;
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
-    if (!ATTN_DMA_G1 && !ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
+    if (!ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
     if (t < nkv) {
       const char* Ks = smem + st * SB;
 #pragma unroll
@@ -370,12 +347,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     // ---------------- Y_t ----------------
-    if (ATTN_DMA_G1) {
-      if (gp == 1 && t + 2 < nkv) dma_all(t + 2, stp);
-    } else {
-      if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
-      if (ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-    }
+    // (waves 4-7 issuing the whole tile t+2 here, waves 0-3 none: 3.9 % slower, the 12 pieces
+    // per wave outgrow the softmax phase; profiles/r03_ab_attn_dma_g1.txt)
+    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
+    if (ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
     if (t < nkv) {
       const int kbase = (t0 + t) * TK;
       auto mask_tail = [&]() {
