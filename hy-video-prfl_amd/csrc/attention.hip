@@ -154,9 +154,11 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // are per-lane 32-bit constants hoisted out of the loop (buffer resources rebased per tile).
 // SCHED > 0 interleaves the LDS reads SCHED+1 MFMAs ahead of their use (sched_group_barrier).
 // SHORT_KV: separate instantiation for the 512/257-key cross-attention (SCHED 1) so profiles
-// separate it from the self-attention (SCHED 2).
+// separate it from the self-attention (ATTN_FWD_SCHED).
+// (3 on the final kernel: -0.6 to -0.9 % vs 2 in two one-process A/Bs, bit-identical:
+// profiles/r03_sweeps_final.txt, r03_ab_attn_sched3.txt)
 #ifndef ATTN_FWD_SCHED
-#define ATTN_FWD_SCHED 2
+#define ATTN_FWD_SCHED 3
 #endif
 // 1: waves 0-3 issue their half of tile t+1 in Y_t (their softmax phase, VALU only) instead of
 // X_t, beside MFMAs and LDS reads where an LDS-DMA piece costs 2-3x the issue cycles (MI355X

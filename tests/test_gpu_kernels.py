@@ -285,7 +285,7 @@ def _lse2_ref(q, k, H, klen, scale):
 @pytest.mark.parametrize("Lq,Lk,H,klen", [(4200, 4200, 2, 4133), (4133, 4133, 1, 4133),
                                           (1000, 4100, 2, 4097), (4111, 5000, 1, 4500)])
 def test_attention_long_kv_vs_oracle(ops, Lq, Lk, H, klen):
-    """The production self-attention instantiation (Lk >= 4096 -> attn_fwd_kernel<false, 2, 3>,
+    """The production self-attention instantiation (Lk >= 4096 -> attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, QS>,
     the L x L forward of every block) and both backward kernels vs the CPU oracle: L not a
     multiple of 96 or 256 (the clamped last K/V tile, partial query tiles), k_len < Lk."""
     g = torch.Generator().manual_seed(Lq * 3 + Lk)
