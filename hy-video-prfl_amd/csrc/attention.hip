@@ -157,6 +157,9 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // separate it from the self-attention (ATTN_FWD_SCHED).
 // (3 on the final kernel: -0.6 to -0.9 % vs 2 in two one-process A/Bs, bit-identical:
 // profiles/r03_sweeps_final.txt, r03_ab_attn_sched3.txt)
+#ifndef ATTN_SHORT_SCHED
+#define ATTN_SHORT_SCHED 1
+#endif
 #ifndef ATTN_FWD_SCHED
 #define ATTN_FWD_SCHED 3
 #endif
@@ -1549,9 +1552,9 @@ int attn_fwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
       hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, false>), grid, dim3(512), 0, s, a);
   } else {
     if (l2q)
-      hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<true, ATTN_SHORT_SCHED, 3, true>), grid, dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_fwd_kernel<true, 1, 3, false>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<true, ATTN_SHORT_SCHED, 3, false>), grid, dim3(512), 0, s, a);
   }
   if (split > 1) hipLaunchKernelGGL(attn_merge_kernel, dim3((unsigned)rem, 8), dim3(256), 0, s, a);
   prfl_prof::set_work(4.0 * B * H * HD * (double)Lq * (double)k_len);

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--L", type=int, default=73920)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--lk", type=int, default=0, help="key count (cross-attention: 512); default L")
     ap.add_argument("--fp8", action="store_true", help="time prfl_attn_fwd_fp8 (config C5) instead")
     ap.add_argument("--qs", default="", help="comma list of lib indices built with ATTN_QS=1: they "
                     "get q pre-scaled by softmax_scale * log2(e) (rounded to bf16 once)")
@@ -26,6 +27,8 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     qkv = torch.randn(L, 3 * C, generator=g, device=dev).to(torch.bfloat16)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    Lk = a.lk or L
+    k, v = k[:Lk], v[:Lk]
     do = torch.randn(L, C, generator=g, device=dev).to(torch.bfloat16)
     outs = [dict(o=torch.empty(L, C, dtype=torch.bfloat16, device=dev), lse=torch.empty(H, L, device=dev),
                  delta=torch.empty(H, L, device=dev), dq=torch.empty(L, C, dtype=torch.bfloat16, device=dev),
@@ -39,14 +42,14 @@ def main():
     def fwd(lib, b):
         qq = (qsc.data_ptr(), C, 0) if b.get("qs") else (q.data_ptr(), 3 * C, 0)
         args = (*qq, k.data_ptr(), 3 * C, 0, v.data_ptr(), 3 * C, 0,
-                b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, L, H, L, sc)
+                b["o"].data_ptr(), C, 0, b["lse"].data_ptr(), 1, L, Lk, H, Lk, sc)
         if a.fp8:
             nb = lib.prfl_attn_fwd_fp8_ws_bytes(1, L, L, H, L)
             if "ws8" not in b or b["ws8"].numel() < nb:
                 b["ws8"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
             assert lib.prfl_attn_fwd_fp8(*args, b["ws8"].data_ptr(), nb, st) == 0
         elif lib.has_ws:
-            nb = lib.prfl_attn_fwd_ws_bytes(1, L, L, H, L)
+            nb = lib.prfl_attn_fwd_ws_bytes(1, L, Lk, H, Lk)
             if "ws" not in b or b["ws"].numel() < nb:
                 b["ws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
             if b.get("qs") and lib.has_l2q:
@@ -77,7 +80,7 @@ def main():
 
     for i in qs_libs:
         outs[i]["qs"] = True
-    work = [("fwd", fwd, 4 * L * L * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
+    work = [("fwd", fwd, 4 * L * Lk * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
     for w, fn, fl in work:
         ts = [[] for _ in libs]
         for r in range(a.reps + 1):
