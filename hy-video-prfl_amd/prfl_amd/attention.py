@@ -9,6 +9,8 @@ import torch
 
 from . import custom_ops
 
+__all__ = ["flash_attention", "attention"]        # attention.py:18-21
+
 
 def flash_attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=None,
                     q_scale=None, causal=False, window_size=(-1, -1), deterministic=False,

@@ -106,3 +106,26 @@ def get_dit_fsdp_kwargs(transformer, sharding_strategy, use_lora=False, cpu_offl
                         else None),
     }
     return kwargs, no_split_modules
+
+
+def get_discriminator_fsdp_kwargs(master_weight_type="fp32"):
+    """`fsdp_utils.py:125-140`: an unwrapped, unsharded FSDP unit for small side models."""
+    return {"auto_wrap_policy": None,
+            "mixed_precision": get_mixed_precision(master_weight_type),
+            "sharding_strategy": ShardingStrategy.NO_SHARD,
+            "device_id": torch.cuda.current_device(),
+            "limit_all_gathers": True}
+
+
+def get_vae_fsdp_kwargs(master_weight_type="fp32", cpu_offload=False):
+    """`fsdp_utils.py:141-168`: the frozen VAE as one FULL_SHARD unit with original parameters
+    (the VAE itself is outside this repo's scope; the keyword set is provided so the PRFL driver's
+    import line and its `FSDP(vae, **get_vae_fsdp_kwargs(...))` call stay unchanged)."""
+    return {"auto_wrap_policy": None,
+            "mixed_precision": get_mixed_precision(master_weight_type),
+            "sharding_strategy": ShardingStrategy.FULL_SHARD,
+            "device_id": torch.cuda.current_device(),
+            "limit_all_gathers": True,
+            "cpu_offload": (torch.distributed.fsdp.CPUOffload(offload_params=True) if cpu_offload
+                            else None),
+            "use_orig_params": True}

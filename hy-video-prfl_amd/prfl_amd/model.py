@@ -25,7 +25,7 @@ from . import ops
 from .linear import linear_bf16
 
 __all__ = ["WanModel", "WanAttentionBlock", "WanRMSNorm", "WanLayerNorm", "rope_params",
-           "rope_apply", "sinusoidal_embedding_1d"]
+           "rope_apply", "sinusoidal_embedding_1d", "pad_freqs"]
 
 T5_CONTEXT_TOKEN_NUMBER = 512
 FIRST_LAST_FRAME_CONTEXT_TOKEN_NUMBER = 257 * 2
@@ -45,6 +45,15 @@ def rope_params(max_seq_len, dim, theta=10000):
     f = torch.outer(torch.arange(max_seq_len, dtype=torch.float64),
                     1.0 / torch.pow(theta, torch.arange(0, dim, 2, dtype=torch.float64).div(dim)))
     return torch.polar(torch.ones_like(f), f)
+
+
+def pad_freqs(original_tensor, target_len):
+    """model.py:45-58: extend per-token rotations [S, n, d] to `target_len` rows with unit
+    multipliers (the sequence-parallel tail).  The reference's diagnostic print reads `pad_size`
+    before assigning it, so its padding branch raises; the intended padding is returned here."""
+    s, a, b = original_tensor.shape
+    pad = original_tensor.new_ones(max(target_len - s, 0), a, b)
+    return torch.cat([original_tensor, pad], dim=0)
 
 
 def rope_apply(x, grid_sizes, freqs):

@@ -100,9 +100,80 @@ class MLP(nn.Module):
         return linear_bf16(x, self.fc3.weight, self.fc3.bias)
 
 
+class MultiHead(nn.Module):
+    """network.py:136-149: `num_heads` independent reward MLPs over one feature; forward returns
+    the stacked sigmoid scores [num_heads, ..., 1]."""
+
+    def __init__(self, input_dim, num_heads=3):
+        super().__init__()
+        self.num_heads = num_heads
+        self.mlps = nn.ModuleList(MLP(input_dim) for _ in range(num_heads))
+
+    def forward_mlp(self, head_idx, x):
+        return torch.sigmoid(self.mlps[head_idx](x))
+
+    def forward(self, x):
+        return torch.stack([self.forward_mlp(h, x) for h in range(self.num_heads)])
+
+
 def forward_mlp(model, input):
     return torch.sigmoid(model(input))
 
 
 def forward_siamese(model, input1, input2):
     return torch.sigmoid(model(input1) - model(input2))
+
+
+def _scores(model, model_mode, X):
+    if model_mode == "clf":
+        return forward_mlp(model, X)
+    if model_mode == "siamese":                   # X [N, 2, ...]: pair (preferred, other)
+        return forward_siamese(model, X[:, 0], X[:, 1])
+    raise ValueError(f"model_mode must be 'clf' or 'siamese', got {model_mode!r}")
+
+
+def train_model(model, device, model_mode, X_train, y_train, X_test, y_test, epochs=3, lr=0.001,
+                batch_size=512, verbose=False, ealry_stopping_patience=3):
+    """network.py:164-214: fit a reward MLP on cached features with Adam + BCE.
+
+    Each epoch runs ceil(N / batch_size) steps, every step on a fresh random subset of
+    `batch_size` rows (drawn with torch.randperm, so it follows the global torch seed as the
+    reference does); after the epoch the validation BCE is recorded and training stops once it
+    exceeds each of the previous `ealry_stopping_patience` values (the reference's spelling of
+    the keyword is kept so callers passing it by name still work).  Returns the model (the
+    reference returns None; callers ignore the result)."""
+    model = model.to(device)
+    bce = nn.BCELoss()
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    n = X_train.shape[0]
+    batch_size = min(batch_size, n)
+    history = []
+    for epoch in range(epochs):
+        model.train()
+        loss = None
+        for _ in range(0, n, batch_size):
+            pick = torch.randperm(n)[:batch_size]
+            opt.zero_grad()
+            loss = bce(_scores(model, model_mode, X_train[pick]), y_train[pick])
+            loss.backward()
+            opt.step()
+        model.eval()
+        with torch.no_grad():
+            val = _scores(model, model_mode, X_test)
+        val_loss = float(bce(val, y_test))
+        history.append(val_loss)
+        p = ealry_stopping_patience
+        if len(history) > p and all(history[-1] > h for h in history[-(p + 1):-1]):
+            if verbose:
+                print(f"Early stopping at epoch {epoch + 1}")
+            break
+        if verbose:
+            acc = ((val > 0.5).to(y_test.dtype) == y_test).float().mean().item()
+            print(f"Epoch {epoch + 1}/{epochs}, Loss: {float(loss)}, Val Loss: {val_loss}")
+            print(f"Accuracy: {acc}")
+    return model
+
+
+def save_model(model, path):
+    """network.py:216-217."""
+    torch.save(model.state_dict(), path)

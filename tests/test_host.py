@@ -53,14 +53,88 @@ def test_real_config_param_count():
     assert abs(nb / 1e6 - 351.4) < 0.5
 
 
-def test_import_shim():
-    from diffusers_lite.wan.modules.model import WanModel, WanAttentionBlock  # noqa: F401
-    from diffusers_lite.utils.network import QueryAttention, MLP, forward_mlp  # noqa: F401
-    from diffusers_lite.wan.utils.fm_solvers_unipc import FlowUniPCMultistepScheduler  # noqa: F401
-    from diffusers_lite.schedulers import FlowMatchDiscreteScheduler  # noqa: F401
-    from diffusers_lite.wan.modules.attention import flash_attention  # noqa: F401
+def _driver_imports():
+    import json
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "driver_imports.json")))
+
+
+def test_dropin_resolves_every_reference_import(monkeypatch):
+    """After `prfl_amd.dropin.install()` (the INTEGRATION.md preamble), every `from <replaced
+    module> import <name>` anywhere in the reference — train_prfl.py:29-97, train_pavrm.py:28-74,
+    inference_pavrm.py, the package's own relative imports — resolves (VERDICT r03 missing #1:
+    train_model / save_model / get_vae_fsdp_kwargs were absent and the drivers died on import)."""
+    import sys
+    from prfl_amd import dropin
+    table = _driver_imports()
+    assert set(table) == set(dropin.MODULE_MAP)
+    for ref_name in dropin.MODULE_MAP:
+        monkeypatch.delitem(sys.modules, ref_name, raising=False)
+    dropin.install()
+    n = 0
+    for mod, entry in table.items():
+        for name, sites in entry["imported"].items():
+            ns = {}
+            exec(f"from {mod} import {name}", ns)        # the driver's own statement form
+            assert ns[name] is not None, (mod, name, sites)
+            n += 1
+    assert n >= 15
+    for ref_name in dropin.MODULE_MAP:
+        monkeypatch.delitem(sys.modules, ref_name, raising=False)
+    from diffusers_lite.wan.modules.model import WanModel
     assert WanModel._no_split_modules == ["WanAttentionBlock"]
     assert WanModel.enable_teacache is False
+
+
+def test_dropin_modules_define_every_reference_name():
+    """Each replacement module exports every top-level name its reference module defines."""
+    import importlib
+    from prfl_amd import dropin
+    for ref_name, entry in _driver_imports().items():
+        ours = importlib.import_module(dropin.MODULE_MAP[ref_name])
+        missing = [x for x in entry["defined"] if not hasattr(ours, x)]
+        assert not missing, (ref_name, missing)
+
+
+def test_driver_imports_fixture_is_current():
+    """The committed fixture equals a fresh parse of the reference sources (skipped where the
+    reference is absent, e.g. on the GPU box)."""
+    import importlib.util
+    import json
+    if not os.path.isdir("/root/reference/scripts"):
+        pytest.skip("reference sources not present")
+    spec = importlib.util.spec_from_file_location(
+        "mdi", os.path.join(ROOT, "tests", "golden", "make_driver_imports.py"))
+    mdi = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mdi)
+    fresh = {}
+    for ref_mod in mdi.MODULE_MAP:
+        path = os.path.join(mdi.REF, *ref_mod.split(".")) + ".py"
+        fresh[ref_mod] = mdi.defined_names(path)
+    table = _driver_imports()
+    assert {k: v["defined"] for k, v in table.items()} == fresh
+    assert json.dumps(table["diffusers_lite.utils.network"]["imported"]).count("train_prfl.py") >= 6
+
+
+def test_train_model_and_save_model(tmp_path):
+    """network.train_model / save_model (network.py:164-217) on a plain torch classifier, both
+    modes; the reward MLPs themselves run on the GPU GEMM."""
+    from prfl_amd.network import save_model, train_model
+    torch.manual_seed(0)
+    X = torch.randn(256, 8)
+    y = (X[:, :1] > 0).float()
+    for mode, Xt in (("clf", X), ("siamese", torch.stack([X, -X], dim=1))):
+        m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+        before = torch.nn.functional.binary_cross_entropy(
+            torch.sigmoid(m(X) - (m(-X) if mode == "siamese" else 0)), y).item()
+        out = train_model(m, "cpu", mode, Xt, y, Xt, y, epochs=20, lr=1e-2, batch_size=64)
+        after = torch.nn.functional.binary_cross_entropy(
+            torch.sigmoid(m(X) - (m(-X) if mode == "siamese" else 0)), y).item()
+        assert out is m and after < 0.6 * before, (mode, before, after)
+        save_model(m, tmp_path / f"{mode}.ckpt")
+        sd = torch.load(tmp_path / f"{mode}.ckpt", weights_only=True)
+        assert all(torch.equal(sd[k], v) for k, v in m.state_dict().items())
+    with pytest.raises(ValueError):
+        train_model(m, "cpu", "ranking", X, y, X, y, epochs=1)
 
 
 def test_unipc_product_vs_reference(golden):
