@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(256) void attn_lp_vamax_kernel(AttnF8Args f) {
   const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * 256;
   const int ch = threadIdx.x & 15, rg = threadIdx.x >> 4;
   float vm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = k0 + rg; r < min(k0 + 256, a.Lk); r += 16) {
+  for (int r = k0 + rg; r < min(k0 + 256, a.k_len); r += 16) {   // masked keys set no scale
     const bf16x8 vv = *(const bf16x8*)(a.V + b * a.bv + (int64_t)r * a.ldv + h * HD + ch * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) vm[j] = fmaxf(vm[j], fabsf(bf2f(vv[j])));
@@ -1140,13 +1140,13 @@ __global__ __launch_bounds__(256) void attn_lp_quant_kernel(AttnF8Args f) {
   __shared__ float kred[4];
   {
     const bf16* src = a.K + b * a.bk + (int64_t)min(row, a.Lk - 1) * a.ldk + h * HD + hf * 64;
-    float am = row < a.Lk ? amax64(src) : 0.f;
+    float am = row < a.k_len ? amax64(src) : 0.f;        // masked keys (>= k_len) set no scale
     am = wave_max(am);
     if ((threadIdx.x & 63) == 0) kred[threadIdx.x >> 6] = am;
     __syncthreads();
     am = fmaxf(fmaxf(kred[0], kred[1]), fmaxf(kred[2], kred[3]));
-    if (row < a.Lk)
-      quant64_i8(src, am > 0.f ? I8_QMAX / am : 0.f,
+    if (row < a.Lk)                                       // and are stored as zeros
+      quant64_i8(src, row < a.k_len && am > 0.f ? I8_QMAX / am : 0.f,
                  (int8_t*)f.K8 + ((int64_t)b * a.Lk + row) * ld8 + h * HD + hf * 64);
     if (threadIdx.x == 0)
       ((float*)f.sk)[((int64_t)b * a.H + h) * (f.lkp >> 7) + blockIdx.x] = am > 0.f ? am / I8_QMAX : 1.f;
@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(256) void attn_lp_quant_kernel(AttnF8Args f) {
   {
     const unsigned* vam = f.vamax + ((int64_t)b * a.H + h) * HD + hf * 64;
     const int key = row - r0, pos = 64 * (key >> 6) + fp8_vt_pos(key & 63);
-    const bool live = row < a.Lk;
+    const bool live = row < a.k_len;     // masked keys -> 0 (their P is 0; 0 x e4m3 NaN is not)
     const bf16* src = a.V + b * a.bv + (int64_t)min(row, a.Lk - 1) * a.ldv + h * HD + hf * 64;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -1656,9 +1656,10 @@ int attn_fwd_fp8_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int
                (const float*)(w + l.sk), (const uint8_t*)(w + l.vt8),
                (const unsigned*)(w + l.vam), l.lkp};
   hipStream_t s = (hipStream_t)stream;
+  const hipError_t ms = hipMemsetAsync(w + l.vam, 0, B * H * HD * 4, s);
+  if (ms != hipSuccess) return (int)ms;
   prfl_prof::begin(KID_ELTWISE, s);
-  if (hipMemsetAsync(w + l.vam, 0, B * H * HD * 4, s) != hipSuccess) return (int)hipErrorLaunchFailure;
-  hipLaunchKernelGGL(attn_lp_vamax_kernel, dim3((unsigned)((Lk + 255) / 256), (unsigned)H, (unsigned)B),
+  hipLaunchKernelGGL(attn_lp_vamax_kernel, dim3((unsigned)((k_len + 255) / 256), (unsigned)H, (unsigned)B),
                      dim3(256), 0, s, f);
   hipLaunchKernelGGL(attn_lp_quant_kernel,
                      dim3((unsigned)((std::max(Lq, lkp) + 127) / 128), (unsigned)H, (unsigned)B),

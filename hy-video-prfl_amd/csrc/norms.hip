@@ -362,10 +362,10 @@ extern "C" int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int 
   return 0;
 }
 
-extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
-                                 float eps, const float* rope_tab, int64_t F, int64_t Hg,
-                                 int64_t Wg, void* out, int64_t ldo, float* rstd, float out_scale,
-                                 void* stream) {
+extern "C" int prfl_rms_rope_fwd_scaled(const void* x, int64_t ldx, int64_t L, int64_t C,
+                                        const float* w, float eps, const float* rope_tab,
+                                        int64_t F, int64_t Hg, int64_t Wg, void* out, int64_t ldo,
+                                        float* rstd, float out_scale, void* stream) {
   if (L <= 0) return 0;
   if (bad_c(C)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -381,10 +381,11 @@ extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t 
   return 0;
 }
 
-extern "C" int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
-                                 const float* rstd, int64_t L, int64_t C, const float* w,
-                                 const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                                 int64_t lddx, float* part0, float out_scale, void* stream) {
+extern "C" int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const void* x,
+                                        int64_t ldx, const float* rstd, int64_t L, int64_t C,
+                                        const float* w, const float* rope_tab, int64_t F,
+                                        int64_t Hg, int64_t Wg, void* dx, int64_t lddx,
+                                        float* part0, float out_scale, void* stream) {
   if (L <= 0) return 0;
   if (bad_c(C)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -397,4 +398,19 @@ extern "C" int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, 
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+
+// the round-2 ABI (no out_scale), kept so callers built against it keep working
+extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
+                                 float eps, const float* rope_tab, int64_t F, int64_t Hg,
+                                 int64_t Wg, void* out, int64_t ldo, float* rstd, void* stream) {
+  return prfl_rms_rope_fwd_scaled(x, ldx, L, C, w, eps, rope_tab, F, Hg, Wg, out, ldo, rstd, 1.f,
+                                  stream);
+}
+extern "C" int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
+                                 const float* rstd, int64_t L, int64_t C, const float* w,
+                                 const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
+                                 int64_t lddx, float* part0, void* stream) {
+  return prfl_rms_rope_bwd_scaled(dout, lddo, x, ldx, rstd, L, C, w, rope_tab, F, Hg, Wg, dx, lddx,
+                                  part0, 1.f, stream);
 }

@@ -194,7 +194,7 @@ def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None, out_sc
         out = torch.empty(L, C, dtype=BF16, device=x.device)
     rstd = torch.empty(L, dtype=torch.float32, device=x.device)
     f, h, ww = grid
-    call("prfl_rms_rope_fwd", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps), ptr(rope_tab),
+    call("prfl_rms_rope_fwd_scaled", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps), ptr(rope_tab),
          I64(f), I64(h), I64(ww), ptr(out), I64(_ld(out)), ptr(rstd), F32(out_scale), stream_ptr())
     return out, rstd
 
@@ -207,7 +207,7 @@ def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_s
     if dx is None:
         dx = torch.empty(L, C, dtype=BF16, device=x.device)
     f, h, ww = grid
-    call("prfl_rms_rope_bwd", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd), I64(L),
+    call("prfl_rms_rope_bwd_scaled", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd), I64(L),
          I64(C), ptr(w), ptr(rope_tab), I64(f), I64(h), I64(ww), ptr(dx), I64(_ld(dx)), ptr(p0),
          F32(out_scale), stream_ptr())
     return dx, colsum_reduce(p0)

@@ -87,7 +87,8 @@ int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k, 
  * and channel, V stored transposed) into the REQUIRED caller-owned scratch `ws` (256-B aligned)
  * of prfl_attn_fwd_fp8_ws_bytes(...) bytes; o and lse2 as prfl_attn_fwd_ws (lse2 is the LSE of
  * the dequantised scores, usable by prfl_attn_bwd).  There is no fp8 flash-attn in the
- * reference: its attention stays bf16 (attention.py:113-127) and fp8 covers its linears. */
+ * reference, which is bf16 throughout (attention.py:113-127; no fp8 anywhere).  Q.K^T runs on the
+ * int8 MFMA, P.V on the e4m3 MFMA. */
 int prfl_attn_fwd_fp8(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
                       int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
                       int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
@@ -174,15 +175,23 @@ int prfl_norm_rows_per_part(void);
  * model.py:61-103; rope_tab = fp32 (cos,sin) [1024][64] of the complex freqs of model.py:521-526,
  * grid (F,Hg,Wg); rows >= F*Hg*Wg are not rotated; rope_tab == NULL -> no RoPE).
  *   out = bf16(rope(bf16(x * rsqrt(mean(x^2)+eps)) * w) * out_scale)
- * out_scale = 1 is the reference's norm_q / norm_k; softmax_scale * log2(e) yields the q operand of
- * the *_l2q attention entries.  The backward scales the incoming gradient by out_scale. */
+ * prfl_rms_rope_fwd / _bwd are the reference's norm_q / norm_k (out_scale 1).  The _scaled forms
+ * (added in round 3) multiply the output by out_scale: softmax_scale * log2(e) yields the q operand
+ * of the *_l2q attention entries; the backward scales the incoming gradient by out_scale. */
 int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w, float eps,
                       const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* out,
-                      int64_t ldo, float* rstd, float out_scale, void* stream);
+                      int64_t ldo, float* rstd, void* stream);
 int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
                       const float* rstd, int64_t L, int64_t C, const float* w,
                       const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                      int64_t lddx, float* part0, float out_scale, void* stream);
+                      int64_t lddx, float* part0, void* stream);
+int prfl_rms_rope_fwd_scaled(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
+                             float eps, const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg,
+                             void* out, int64_t ldo, float* rstd, float out_scale, void* stream);
+int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const void* x, int64_t ldx,
+                             const float* rstd, int64_t L, int64_t C, const float* w,
+                             const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
+                             int64_t lddx, float* part0, float out_scale, void* stream);
 
 /* ---- element-wise / reductions ------------------------------------------------------------ */
 /* autocast weight cast fp32 -> bf16 (the .to(bf16) of every Linear weight under autocast). */

@@ -289,6 +289,155 @@ def case_toy_prfl():
         sft_loss=np32(sft_loss), **g_reward, **g_sft)
 
 
+SPLIT_MIDS = (0, 3)
+
+
+def _unipc_state(sch):
+    """The reference scheduler's state before a step: what the grad-enabled step reads."""
+    st = {"state:lon": np.int64(sch.lower_order_nums), "state:this_order": np.int64(getattr(sch, "this_order", 1)),
+          "state:step_index": np.int64(-1 if sch.step_index is None else sch.step_index)}
+    for j, mo in enumerate(sch.model_outputs):
+        if mo is not None:
+            st[f"state:mo{j}"] = np32(mo)
+            st[f"state:mo{j}:bf16"] = np.bool_(mo.dtype == torch.bfloat16)
+    if sch.last_sample is not None:
+        st["state:last"] = np32(sch.last_sample)
+        st["state:last:bf16"] = np.bool_(sch.last_sample.dtype == torch.bfloat16)
+    return st
+
+
+def _toy_prfl_models():
+    gen = _toy_model("t2v")
+    lrm = _toy_model("t2v")
+    lrm.blocks = torch.nn.ModuleList([lrm.blocks[0]])
+    del lrm.head
+    lrm.head = None
+    for p in lrm.parameters():
+        p.requires_grad_(False)
+    qa = load_seeded(NET.QueryAttention(256, 1, 8, 0., return_type="query"), prefix="tqa.")
+    mlp = load_seeded(NET.MLP(256), prefix="tmlp.")
+    for p in list(qa.parameters()) + list(mlp.parameters()):
+        p.requires_grad_(False)
+    return gen, lrm, qa, mlp
+
+
+def _lrm_pool(lrm, qa, stepped, t1, ctx, ac):
+    """LRM feature tap + QueryAttention (`train_prfl.py:745-790`) from a leaf copy of the stepped
+    latent: (leaf, pooled)."""
+    leaf = stepped.detach().clone().requires_grad_(True)
+    with torch.autocast(**ac):
+        feats = DU.list2batch(lrm(x=DU.batch2list(leaf), t=t1, context=DU.batch2list(ctx),
+                                  seq_len=105, output_features=True, selected_layers=[1]))
+        pooled = qa(feats)
+    return leaf, pooled
+
+
+def _mlp_hinge(mlp, pooled, ac):
+    """MLP + sigmoid + hinge / GA (`train_prfl.py:791-798`, GA 5) from a leaf copy of the
+    pooled feature: (loss, reward, d loss / d pooled)."""
+    p = pooled.detach().clone().requires_grad_(True)
+    with torch.autocast(**ac):
+        r = NET.forward_mlp(mlp, p)
+        loss = 0.1 * torch.relu(-r.squeeze() + 2).mean()
+    loss = loss / 5.0
+    loss.backward()
+    return loss, r, p.grad
+
+
+def case_toy_prfl_split():
+    """The reward chain of `train_prfl.py:703-830` cut at the pooled feature and at the stepped
+    latent, so each piece is pinned on the reference's own inputs, without the bf16 noise of the
+    pieces before it:
+
+    * head: MLP + sigmoid + hinge from the reference's pooled feature -> d(pooled).  This is the
+      one non-smooth piece: its ReLUs switch for units within a bf16 ulp of zero, which is what
+      makes whole-chain bf16 runs land 1-8 % apart (the reference's own bf16 head is 4.6-7.5 %
+      from its fp32 evaluation on the same input);
+    * trunk: LRM + QueryAttention backward from the reference's stepped bf16 latent with the
+      reference's d(pooled) upstream -> d(stepped) (smooth: the reference is 0.5 % from the fp32
+      truth here);
+    * generator: the grad-enabled generator step + differentiable UniPC step from the
+      reference's pre-step latent and scheduler state, back-propagating the reference's
+      d(stepped) -> every generator gradient.
+
+    Cutting does not change the reference's arithmetic: the gradients reaching the pooled feature
+    and the bf16 stepped latent are the same tensors as in the uncut backward.  Each piece also
+    has its fp32 truth on the same inputs.  Two mids: 0 (no rollout, order-1 step, no corrector)
+    and 3 (corrector + order-2 predictor from the rollout's history)."""
+    ctx = torch.from_numpy(seeded.randn("prfl.ctx", (1, 20, TOY["text_dim"]))).to(torch.bfloat16)
+    out = {"ctx": np32(ctx)}
+    no_ac = dict(AC, enabled=False)
+    for mid in SPLIT_MIDS:
+        pre = f"m{mid}:"
+        gen, lrm, qa, mlp = _toy_prfl_models()
+        sch = UNIPC.FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                                use_dynamic_shifting=False)
+        sch.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
+        ts = sch.timesteps
+        latent = torch.from_numpy(seeded.randn("prfl.noise", (1,) + TOY_LATENT)).to(torch.bfloat16)
+        with torch.no_grad():
+            for i in range(mid):
+                with torch.autocast(**AC):
+                    npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[i]]),
+                                              context=DU.batch2list(ctx), seq_len=105))
+                    latent = sch.step(npred, ts[i], latent, return_dict=False)[0]
+        state = _unipc_state(sch)
+        pre_lat = latent.clone()
+        with torch.autocast(**AC):
+            npred = DU.list2batch(gen(x=DU.batch2list(latent), t=torch.tensor([ts[mid]]),
+                                      context=DU.batch2list(ctx), seq_len=105))
+        stepped = sch.step(npred, ts[mid], latent, return_dict=False)[0]
+        t1 = torch.tensor([ts[mid + 1]])
+        leaf, pooled = _lrm_pool(lrm, qa, stepped, t1, ctx, AC)
+        loss, r, dpool = _mlp_hinge(mlp, pooled, AC)
+        pooled.backward(dpool)                                   # the trunk piece
+        dstep = leaf.grad
+        stepped.backward(dstep)                                  # the generator piece
+        g_gen = grads_of(gen, head=4096, full_max=4096)
+        # fp32 truths of each piece on the same inputs and upstream gradients
+        saved = M.flash_attention
+        M.flash_attention = _exact_attention
+        try:
+            gen32, lrm32, qa32, mlp32 = _toy_prfl_models()
+            _, r32, dpool32 = _mlp_hinge(mlp32, pooled.float(), no_ac)
+            leaf32, pooled32 = _lrm_pool(lrm32, qa32, stepped.float(), t1, ctx.float(), no_ac)
+            pooled32.backward(dpool.float())
+            dstep32 = leaf32.grad
+            sch32 = UNIPC.FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                                      use_dynamic_shifting=False)
+            sch32.set_timesteps(num_inference_steps=40, device="cpu", shift=5.0)
+            sch32.model_outputs = [None if k not in state else torch.from_numpy(state[k])
+                                   for k in ("state:mo0", "state:mo1")]
+            sch32.last_sample = (torch.from_numpy(state["state:last"]) if "state:last" in state
+                                 else None)
+            sch32.lower_order_nums = int(state["state:lon"])
+            sch32.this_order = int(state["state:this_order"])
+            if int(state["state:step_index"]) >= 0:
+                sch32._step_index = int(state["state:step_index"])
+            npred32 = DU.list2batch(gen32(x=DU.batch2list(pre_lat.float()),
+                                          t=torch.tensor([ts[mid]]),
+                                          context=DU.batch2list(ctx.float()), seq_len=105))
+            stepped32 = sch32.step(npred32, ts[mid], pre_lat.float(), return_dict=False)[0]
+            stepped32.backward(dstep.float())
+            g_gen32 = grads_of(gen32, head=4096, full_max=4096)
+        finally:
+            M.flash_attention = saved
+        e = lambda a, b: ((a.float() - b).norm() / b.norm()).item()  # noqa: E731
+        print(f"mid {mid}: reward {r.item():.5f} (truth {r32.item():.5f}); reference vs truth: "
+              f"d(pooled) {e(dpool, dpool32):.4f}, d(stepped) {e(dstep, dstep32):.4f}")
+        out.update({pre + "pre": np32(pre_lat), pre + "npred": np32(npred),
+                    pre + "stepped": np32(stepped), pre + "t_mid": np.int64(ts[mid]),
+                    pre + "t1": np.int64(ts[mid + 1]), pre + "loss": np32(loss),
+                    pre + "reward": np32(r), pre + "pooled": np32(pooled),
+                    pre + "dpool": np32(dpool), pre + "dstep": np32(dstep),
+                    pre + "t32:dpool": np32(dpool32), pre + "t32:dstep": np32(dstep32),
+                    pre + "t32:reward": np32(r32),
+                    **{pre + k: v for k, v in state.items()},
+                    **{pre + k: v for k, v in g_gen.items()},
+                    **{pre + "t32:" + k: v for k, v in g_gen32.items()}})
+    save("toy_prfl_split", **out)
+
+
 def case_toy_pavrm():
     """Toy PAVRM training step with the 'ce' loss, restating `train_pavrm.py:671-920` on the
     reference modules: `model_init` (`:200-235`: embeddings frozen, trainable_blocks kept, head
@@ -383,7 +532,7 @@ def _bump_ulps(t, name, n=8):
     return bits.view(torch.bfloat16).view(t.shape).to(t.dtype)
 
 
-def _trainer_run(truth, perturb=None):
+def _trainer_run(truth, perturb=None, mids=TRAINER_MID):
     """Two PRFL iterations (step 0, then step 1 = an optimizer-step boundary for
     gradient_accumulation_steps 2) restating `train_prfl.py` on the reference modules:
     `train_step` (`:900-980`: flow-matching SFT loss / GA, backward, `clip_grad_norm_(1.0)`,
@@ -466,7 +615,7 @@ def _trainer_run(truth, perturb=None):
                 .to(torch.bfloat16).to(lat_dt)
             if perturb is not None:
                 latent = _bump_ulps(latent, f"trainer.perturb.{perturb}.{step}")
-            mid = TRAINER_MID[step]
+            mid = mids[step]
             with torch.no_grad():
                 for i in range(mid):
                     with torch.autocast(**ac):
@@ -508,18 +657,19 @@ def _fresh_err_stats(run, t32, tag):
 TRAINER_PERTURB = 8
 
 
-def case_toy_prfl_trainer():
+def case_toy_prfl_trainer(mids=TRAINER_MID, name="toy_prfl_trainer"):
     """PRFLTrainer parity: the reference run, its fp32 truth, and the reference's
     own bf16 noise floor through the reward chain: TRAINER_PERTURB more reference runs whose
-    reward-step initial noise differs by one bf16 ulp in 8 elements (the chain amplifies state
-    perturbations at bf16 resolution ~10x, so one bf16 run's distance to the truth is a draw from
-    this spread, not a fixed number)."""
-    ref = _trainer_run(truth=False)
-    t32 = _trainer_run(truth=True)
+    reward-step initial noise differs by one bf16 ulp in 8 elements (the chain's MLP ReLUs switch
+    at bf16 resolution, case_toy_prfl_split, so one bf16 run's distance to the truth is a draw
+    from this spread, not a fixed number).  `mids` = the reward steps' mid_timestep per
+    iteration; the `_mid0` fixture runs both iterations without a rollout."""
+    ref = _trainer_run(truth=False, mids=mids)
+    t32 = _trainer_run(truth=True, mids=mids)
     tags = [f"it{s}:{p}" for s in (0, 1) for p in ("sft", "rwd")]
     floor = {t: [] for t in tags}
     for i in range(TRAINER_PERTURB):
-        run = _trainer_run(truth=False, perturb=i)
+        run = _trainer_run(truth=False, perturb=i, mids=mids)
         for t in tags:
             floor[t].append(_fresh_err_stats(run, t32, t))
     extra = {}
@@ -528,8 +678,8 @@ def case_toy_prfl_trainer():
         extra[f"floor:{t}:max"] = np.asarray([x for _, x in floor[t]])
         print(t, "reference runs' median err vs truth:", np.round(extra[f"floor:{t}:med"], 4),
               "max:", np.round(extra[f"floor:{t}:max"], 4))
-    save("toy_prfl_trainer", ga=np.float64(TRAINER_GA), lr=np.float64(TRAINER_LR),
-         sft_idx=np.asarray(TRAINER_SFT_IDX), mid=np.asarray(TRAINER_MID), **ref,
+    save(name, ga=np.float64(TRAINER_GA), lr=np.float64(TRAINER_LR),
+         sft_idx=np.asarray(TRAINER_SFT_IDX), mid=np.asarray(mids), **ref,
          **{"t32:" + k: v for k, v in t32.items()}, **extra)
 
 
@@ -581,9 +731,13 @@ def _toy_pavrm_fp32_truth(step, states, noisy, timestep, ctx, label):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl", "pavrm", "trainer"]
+    which = sys.argv[1:] or ["ops", "toy", "real", "head", "sched", "prfl", "pavrm", "trainer", "trainer0", "split"]
     if "trainer" in which:
         case_toy_prfl_trainer()
+    if "trainer0" in which:
+        case_toy_prfl_trainer(mids=(0, 0), name="toy_prfl_trainer_mid0")
+    if "split" in which:
+        case_toy_prfl_split()
     if "pavrm" in which:
         case_toy_pavrm()
     if "ops" in which:

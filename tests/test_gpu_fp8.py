@@ -223,11 +223,17 @@ def test_block_fp8_vs_fp32_truth():
 
 
 # ------------------------------------------------- low-precision self-attention forward (C5) --
-def _quant_ref(q, k, v, H):
+def _quant_ref(q, k, v, H, klen=None):
     """The kernel's quantisation restated in torch (prfl_attn_fwd_fp8's prologue): Q int8 per
     (token, head) and K int8 per (128-key tile, head), each amax / 127, round to nearest even;
-    V e4m3 per (head, channel), amax / 448.  Returns the DEQUANTISED fp32 operands [H, L, 128]."""
+    V e4m3 per (head, channel), amax / 448; the K / V scales over the keys < klen only (masked
+    keys are quantised to 0).  Returns the DEQUANTISED fp32 operands [H, L, 128]."""
     Lq, Lk = q.shape[0], k.shape[0]
+    klen = Lk if klen is None else klen
+    if klen < Lk:
+        k, v = k.clone(), v.clone()
+        k[klen:] = 0
+        v[klen:] = 0
     qh = q.float().view(Lq, H, 128).transpose(0, 1)
     kh = k.float().view(Lk, H, 128).transpose(0, 1)
     vh = v.float().view(Lk, H, 128).transpose(0, 1)
@@ -281,13 +287,42 @@ def test_attn_fp8_vs_dequantised_fp64(Lq, Lk, H, klen):
     scale = 128 ** -0.5
     o, lse = ops.attn_fwd_fp8(q, k, v, H, k_len=klen)
     torch.cuda.synchronize()
-    qd, kd, vd = _quant_ref(q, k, v, H)
+    qd, kd, vd = _quant_ref(q, k, v, H, klen)
     ro, rlse = _attn64(qd, kd, vd, klen, scale)
     assert torch.isfinite(o).all()
     r = rel(o, ro)
     print(f"vs dequantised fp64: O rel-L2 {r:.3e}, max |dLSE2| {(lse.double() - rlse).abs().max().item():.2e}")
     assert r < 2.5e-2, r
     assert (lse.double() - rlse).abs().max().item() < 5e-2
+
+
+@pytest.mark.parametrize("Lq,Lk,klen", [(1000, 4100, 3990), (600, 777, 700)])
+def test_attn_fp8_masked_keys_set_no_scale(Lq, Lk, klen):
+    """Keys at or past k_len (padding) set none of the C5 quantisation scales: with
+    the padding rows 1000 x larger than the valid keys, the output and LSE are bit-identical to
+    those of zero padding, and match fp64 attention over the operands quantised from the valid
+    keys alone."""
+    from prfl_amd import ops
+    H = 2
+    g = torch.Generator(device=DEV).manual_seed(Lk + klen)
+    C = H * 128
+    q = torch.randn(Lq, C, generator=g, device=DEV).to(torch.bfloat16)
+    k = torch.randn(Lk, C, generator=g, device=DEV).to(torch.bfloat16)
+    v = torch.randn(Lk, C, generator=g, device=DEV).to(torch.bfloat16)
+    k0, v0 = k.clone(), v.clone()
+    k0[klen:] = 0
+    v0[klen:] = 0
+    kb, vb = k0.clone(), v0.clone()
+    kb[klen:] = 1000 * torch.randn(Lk - klen, C, generator=g, device=DEV).to(torch.bfloat16)
+    vb[klen:] = 1000 * torch.randn(Lk - klen, C, generator=g, device=DEV).to(torch.bfloat16)
+    o0, l0 = ops.attn_fwd_fp8(q, k0, v0, H, k_len=klen)
+    ob, lb = ops.attn_fwd_fp8(q, kb, vb, H, k_len=klen)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ob).all()
+    assert torch.equal(o0, ob) and torch.equal(l0, lb)
+    qd, kd, vd = _quant_ref(q, kb, vb, H, klen)
+    ro, _ = _attn64(qd, kd, vd, klen, 128 ** -0.5)
+    assert rel(ob, ro) < 2.5e-2, rel(ob, ro)
 
 
 @pytest.mark.parametrize("L,H", [(4200, 16), (73920, 1)])
