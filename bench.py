@@ -463,7 +463,8 @@ def main():
         "ms_per_step": round(dt / steps * 1e3, 1), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": ("fp8-e4m3 fwd GEMMs / bf16" if args.fp8_gemm_only else
-                  "fp8-e4m3 fwd GEMMs + self-attention fwd / bf16") if args.fp8 else "bf16",
+                  "fp8-e4m3 fwd GEMMs + int8 QK / e4m3 PV self-attention fwd / bf16")
+        if args.fp8 else "bf16",
         "data": "synthetic latents/text, random-init 14B weights",
         "config": {"workload": workload, "model": model, "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},

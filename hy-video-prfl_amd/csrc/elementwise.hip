@@ -146,7 +146,10 @@ __global__ void scale_kernel(float* __restrict__ x, int64_t n, const float* __re
 // torch/optim/adamw.py _single_tensor_adamw semantics (fp32):
 //   p *= 1 - lr*wd ; m += (1-b1)(g-m) ; v = b2 v + (1-b2) g^2
 //   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
-__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+// ZG: the gradient is zeroed once read (optimizer.step() + zero_grad() in one pass, keeping the
+// gradient buffers allocated for the next accumulation)
+template <bool ZG>
+__global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
                              float b1, float b2, float eps, float wd, float step_size,
                              float bc2_sqrt) {
@@ -174,8 +177,12 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     }
     if (cnt == 4) {
       *(f32x4*)(p + i) = pv; *(f32x4*)(m + i) = mv; *(f32x4*)(v + i) = vv;
+      if (ZG) *(f32x4*)(g + i) = (f32x4){0.f, 0.f, 0.f, 0.f};
     } else {
-      for (int j = 0; j < cnt; ++j) { p[i + j] = pv[j]; m[i + j] = mv[j]; v[i + j] = vv[j]; }
+      for (int j = 0; j < cnt; ++j) {
+        p[i + j] = pv[j]; m[i + j] = mv[j]; v[i + j] = vv[j];
+        if (ZG) g[i + j] = 0.f;
+      }
     }
   }
 }
@@ -255,19 +262,38 @@ extern "C" int prfl_scale(float* x, int64_t n, const float* factor, void* stream
   return 0;
 }
 
-extern "C" int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
-                          float beta1, float beta2, float eps, float weight_decay, int64_t step,
-                          void* stream) {
+namespace {
+int adamw_launch(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, int64_t step, bool zero_grad,
+                 void* stream) {
   if (n <= 0) return 0;
   if (step < 1) return (int)hipErrorInvalidValue;
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_ADAMW, s);
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(NT), 0, s, p, g, m, v, n, lr, beta1,
-                     beta2, eps, weight_decay, (float)(lr / bc1), (float)sqrt(bc2));
-  prfl_prof::set_work((double)n * 28.0);
+  if (zero_grad)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid_for(n)), dim3(NT), 0, s, p, g, m, v, n, lr,
+                       beta1, beta2, eps, weight_decay, (float)(lr / bc1), (float)sqrt(bc2));
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid_for(n)), dim3(NT), 0, s, p, g, m, v, n, lr,
+                       beta1, beta2, eps, weight_decay, (float)(lr / bc1), (float)sqrt(bc2));
+  prfl_prof::set_work((double)n * (zero_grad ? 32.0 : 28.0));
   prfl_prof::end(KID_ADAMW, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+}  // namespace
+
+extern "C" int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                          float beta1, float beta2, float eps, float weight_decay, int64_t step,
+                          void* stream) {
+  return adamw_launch(p, const_cast<float*>(g), m, v, n, lr, beta1, beta2, eps, weight_decay,
+                      step, false, stream);
+}
+
+extern "C" int prfl_adamw_zero_grad(float* p, float* g, float* m, float* v, int64_t n, float lr,
+                                    float beta1, float beta2, float eps, float weight_decay,
+                                    int64_t step, void* stream) {
+  return adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, true, stream);
 }

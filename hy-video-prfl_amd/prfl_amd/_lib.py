@@ -58,6 +58,7 @@ SIGNATURES = {
     "prfl_sumsq": [P, I64, P, P],
     "prfl_scale": [P, I64, P, P],
     "prfl_adamw": [P, P, P, P, I64, F32, F32, F32, F32, F32, I64, P],
+    "prfl_adamw_zero_grad": [P, P, P, P, I64, F32, F32, F32, F32, F32, I64, P],
     "prfl_quant_rows_fp8": [P, I32, I64, I64, I64, P, I64, P, P],
     "prfl_gemm_fp8": [P, I64, P, P, I64, P, P, I64, I64, I64, I64, I32, P, P, P, I64, I32, P, I64,
                       P],

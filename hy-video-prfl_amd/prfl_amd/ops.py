@@ -337,11 +337,13 @@ def scale_(x, factor):
     call("prfl_scale", ptr(x), I64(x.numel()), ptr(factor), stream_ptr())
 
 
-def adamw_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step):
+def adamw_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, zero_grad=False):
+    """One AdamW step on p (m, v: its moments); zero_grad also sets g to 0 once read."""
     for t in (p, g, m, v):
         assert t.is_contiguous() and t.dtype == torch.float32
-    call("prfl_adamw", ptr(p), ptr(g), ptr(m), ptr(v), I64(p.numel()), F32(lr), F32(beta1),
-         F32(beta2), F32(eps), F32(weight_decay), I64(step), stream_ptr())
+    call("prfl_adamw_zero_grad" if zero_grad else "prfl_adamw", ptr(p), ptr(g), ptr(m), ptr(v),
+         I64(p.numel()), F32(lr), F32(beta1), F32(beta2), F32(eps), F32(weight_decay), I64(step),
+         stream_ptr())
 
 
 def rope_table(freqs_complex, device):

@@ -113,14 +113,23 @@ class AdamW:
 
     # ------------------------------------------------------------------ update ------------
     @torch.no_grad()
-    def step(self):
+    def step(self, zero_grad=False):
+        """One AdamW update of every parameter holding a gradient.  `zero_grad`: the update
+        kernel also zeroes each gradient once read (= step() + zero_grad(set_to_none=False) in
+        one pass): the gradient buffers stay allocated, so the next backward accumulates into
+        them instead of allocating 4 B / parameter again while this update may still be reading
+        the old ones on the side stream (which made the caching allocator reserve a second set)."""
         self.step_count += 1
         lr = self.param_groups[0]["lr"]
         live = [p for p in self.params if p.grad is not None]
         if not live:
             return
         if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
-            return self._step_cpu(live, lr)
+            self._step_cpu(live, lr)
+            if zero_grad:
+                for p in live:
+                    p.grad.zero_()
+            return
         dev = live[0].device
         main = torch.cuda.current_stream(dev)
         if self._streams is None:
@@ -130,10 +139,14 @@ class AdamW:
         opt.wait_stream(main)                       # grads (clipped) and params are final
         mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
         with torch.cuda.stream(opt):
+            if zero_grad and self.shard:            # tensors another rank updates
+                for p in live:
+                    if self.owner[p] != self.rank:
+                        p.grad.zero_()
             if self.state_on_host:
-                done = self._update_streamed(mine, lr, opt, cp)
+                done = self._update_streamed(mine, lr, opt, cp, zero_grad)
             else:
-                done = self._update_device(mine, lr)
+                done = self._update_device(mine, lr, zero_grad)
             if self.shard:
                 import torch.distributed as dist
                 for p in live:
@@ -150,19 +163,21 @@ class AdamW:
         if not self.overlap:
             self.wait(live)
 
-    def _update_device(self, live, lr):
+    def _update_device(self, live, lr, zero_grad=False):
         done = {}
         for p in live:
             m, v = self._state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             ops.adamw_(p.data, g, m, v, lr, self.betas[0], self.betas[1], self.eps,
-                       self.weight_decay, self.step_count)
+                       self.weight_decay, self.step_count, zero_grad=zero_grad)
+            if zero_grad and g is not p.grad:
+                p.grad.zero_()
             ev = torch.cuda.Event()
             ev.record()
             done[p] = ev
         return done
 
-    def _update_streamed(self, live, lr, opt, cp):
+    def _update_streamed(self, live, lr, opt, cp, zero_grad=False):
         """Moments host -> ring -> kernel -> host, one copy stream for both directions: copy
         stream order H2D(0..k-1), then per tensor i: D2H(i) after kernel(i), H2D(i+k) into the
         slot D2H(i) just drained."""
@@ -199,7 +214,10 @@ class AdamW:
             opt.wait_event(h2d_ev[i])
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             ops.adamw_(p.data, g, m_d[:n].view_as(p), v_d[:n].view_as(p), lr, self.betas[0],
-                       self.betas[1], self.eps, self.weight_decay, self.step_count)
+                       self.betas[1], self.eps, self.weight_decay, self.step_count,
+                       zero_grad=zero_grad)
+            if zero_grad and g is not p.grad:
+                p.grad.zero_()
             ev = torch.cuda.Event()
             ev.record(opt)
             done[p] = ev

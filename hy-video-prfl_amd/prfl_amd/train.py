@@ -101,8 +101,7 @@ class PRFLTrainer:
         self.reducer.end()
         grad_norm = clip_grad_norm_(self.params, self.max_grad_norm)
         if (step + 1) % self.grad_accum == 0:
-            self.optimizer.step()
-            self.optimizer.zero_grad()
+            self.optimizer.step(zero_grad=True)       # step + zero_grad (buffers kept)
         return grad_norm
 
     def _kw(self, latent, text_states, seq_len, image_embeds, cond):
@@ -240,8 +239,6 @@ class PAVRMTrainer:
         loss.backward()
         self.reducer.end()
         grad_norm = clip_grad_norm_(self.trunk_params, self.max_grad_norm)
-        self.opt_trunk.step()
-        self.opt_head.step()
-        self.opt_trunk.zero_grad()
-        self.opt_head.zero_grad()
+        self.opt_trunk.step(zero_grad=True)
+        self.opt_head.step(zero_grad=True)
         return dict(loss=all_reduce_mean(loss.detach()), grad_norm=grad_norm, prob=out.detach())

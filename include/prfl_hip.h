@@ -211,6 +211,10 @@ int prfl_scale(float* x, int64_t n, const float* factor, void* stream);
 /* torch.optim.AdamW step (train_prfl.py:485-491, :827-830) on one fp32 tensor. */
 int prfl_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, void* stream);
+/* prfl_adamw + optimizer.zero_grad() in the same pass (train_prfl.py:827-830): g is set to 0
+ * after it is read, so the gradient buffer stays allocated for the next accumulation. */
+int prfl_adamw_zero_grad(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, int64_t step, void* stream);
 
 /* ---- fp8 path (config C5, train_prfl_i2v_720 "fp8 MFMA path"; SURVEY §8c tolerance 5e-2 vs
  * the bf16 path).  The reference itself is bf16-only; these replace the same autocast

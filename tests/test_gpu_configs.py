@@ -1,0 +1,237 @@
+"""Every BASELINE.json configuration at its real width and geometry, through the trainers.
+
+The trainers of `prfl_amd.train` restate `train_pavrm.py:671-920` (PAVRMTrainer.step) and
+`train_prfl.py:585-1034` (PRFLTrainer.sft_step + reward_step).  Here they run on the 14B block
+width (C = 5120, 40 heads, F = 13 824, 4096-wide text, 1280-wide CLIP) at each config's latent
+geometry, with the number of blocks cut to 2 (generator / PAVRM trunk) and 1 (PRFL reward trunk)
+so a test stays within a couple of minutes:
+
+  C2 train_pavrm_t2v_480   480p x 81f, latent [16, 21, 60, 104] -> L = 32 760
+  C3 train_prfl_t2v_480    480p x 81f, L = 32 760
+  C4 train_prfl_t2v_720    720p x 81f, latent [16, 21, 88, 160] -> L = 73 920 (host AdamW moments,
+                           the attention stash: the 720p memory plan's code paths)
+  C5 train_prfl_i2v_720    I2V (36 input channels, 257 CLIP tokens) at 720p x 81f with the fp8
+                           path on (e4m3 projections, int8 Q.K^T / e4m3 P.V self-attention)
+
+(C1, one block forward at 480p x 49f, is test_gpu_block.py::test_c1_block_forward_480p49f_vs_oracle.)
+Each checks: finite losses and gradient norms; every trainable parameter's fresh gradient finite
+and non-zero; the optimizer moved the parameters; and block 0's output during the step, on 1 024
+rows spread over the sequence, against the oracle run on the captured block inputs (keys and
+values from all L tokens): output <= 1e-2 and residual update <= 3e-2 rel-L2 (bf16 configs), and
+for C5 the update held to the fp32 truth within 16 x the bf16 oracle's own error (the rule of
+test_gpu_fp8.py::test_block_fp8_vs_fp32_truth) and 1e-1.
+"""
+import pytest
+import torch
+
+from oracle import wan_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+REAL = dict(dim=5120, ffn_dim=13824, freq_dim=256, text_dim=4096, out_dim=16, num_heads=40)
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu().flatten()
+    b = torch.as_tensor(b).detach().double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def real_models(model_type, gen_layers, lrm_layers, seed=110221):
+    """Random-init real-width models as bench.py builds them (head perturbed)."""
+    from prfl_amd.model import WanModel
+    from prfl_amd.network import MLP, QueryAttention
+    torch.manual_seed(seed)
+    in_dim = 16 if model_type == "t2v" else 36
+    with torch.device(DEV):
+        gen = None
+        if gen_layers:
+            gen = WanModel(model_type=model_type, in_dim=in_dim, num_layers=gen_layers, **REAL)
+            torch.nn.init.normal_(gen.head.head.weight, std=0.02)
+        lrm = WanModel(model_type=model_type, in_dim=in_dim, num_layers=lrm_layers, **REAL)
+        del lrm.head
+        lrm.head = None
+        qa = QueryAttention(5120, 1, 8, 0., return_type="query")
+        mlp = MLP(5120)
+    return gen, lrm, qa, mlp
+
+
+def inputs(Fl, Hl, Wl, i2v=False, seed=7):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    lat = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=DEV).to(torch.bfloat16)
+    text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=DEV)).to(torch.bfloat16)
+    clip = cond = None
+    if i2v:       # train_prfl.py:531-549: CLIP tokens + 4 mask channels + condition latent
+        clip = torch.randn(1, 257, 1280, generator=g, device=DEV).to(torch.bfloat16)
+        cond = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=DEV).to(torch.bfloat16)
+        mask = torch.zeros(1, 4, Fl, Hl, Wl, device=DEV, dtype=torch.bfloat16)
+        mask[:, :, :1] = 1
+        cond = torch.cat([mask, cond], dim=1)
+    return lat, text, clip, cond
+
+
+class BlockCapture:
+    """Forward hook on one WanAttentionBlock: the inputs and output of its first call, on the
+    host (the oracle runs there)."""
+
+    def __init__(self, blk):
+        self.blk, self.got = blk, None
+        self.h = blk.register_forward_hook(self.hook)
+
+    def hook(self, mod, args, out):
+        if self.got is None:
+            x, e, seq_lens, grid, freqs, ctx, _ = args
+            self.got = dict(x=x.detach().cpu(), e=e.detach().cpu(), grid=grid.cpu(),
+                            ctx=ctx.detach().cpu(), out=out.detach().float().cpu(),
+                            params={n: p.detach().float().cpu()
+                                    for n, p in mod.named_parameters()})
+            self.h.remove()
+
+
+def check_block_vs_oracle(cap, i2v=False, fp8=False):
+    """Block 0's output on 1 024 rows (first / last 16 included) vs the oracle on the captured
+    inputs; returns the report."""
+    torch.set_num_threads(16)
+    c = cap.got
+    assert c is not None, "block 0 never ran"
+    L = c["x"].shape[1]
+    rows = torch.cat([torch.arange(0, 16), torch.linspace(16, L - 17, 992).long(),
+                      torch.arange(L - 16, L)])
+    P = {"b." + n: v for n, v in c["params"].items()}
+    x = c["x"]
+
+    def oracle(truth):
+        saved = O.bf
+        if truth:
+            O.bf = lambda t: t
+        try:
+            with torch.no_grad():
+                return O.block_forward(P, "b.", x, c["e"], c["grid"], O.rope_freqs(128),
+                                       c["ctx"].float(), 40, seq_len=L, i2v=i2v, rows=rows)
+        finally:
+            O.bf = saved
+    out = c["out"][:, rows]
+    xr = x[:, rows].float()
+    ref = oracle(False)
+    rep = {"L": L, "out vs oracle": rel(out, ref), "update vs oracle": rel(out - xr, ref - xr)}
+    assert torch.isfinite(c["out"]).all()
+    if fp8:
+        t32 = oracle(True)
+        rep["update vs truth"] = rel(out - xr, t32 - xr)
+        rep["oracle bf16 update vs truth"] = rel(ref - xr, t32 - xr)
+        assert rep["update vs truth"] <= 16 * rep["oracle bf16 update vs truth"], rep
+        assert rep["update vs truth"] < 1e-1 and rep["out vs oracle"] < 1e-2, rep
+    else:
+        assert rep["out vs oracle"] < 1e-2 and rep["update vs oracle"] < 3e-2, rep
+    return rep
+
+
+def fresh_grad_recorder(reducer, params):
+    """Wraps GradReducer.begin / end to record each backward's fresh gradients' health."""
+    rec = []
+    begin, end = reducer.begin, reducer.end
+    state = {}
+
+    def b():
+        state["before"] = [p.grad.clone() if p.grad is not None else None for p in params]
+        begin()
+
+    def e():
+        end()
+        bad, zero = 0, 0
+        for p, g0 in zip(params, state["before"]):
+            g = p.grad if g0 is None else p.grad - g0
+            if g is None or not torch.isfinite(g).all():
+                bad += 1
+            elif not bool(g.abs().sum() > 0):
+                zero += 1
+        rec.append((bad, zero))
+    reducer.begin, reducer.end = b, e
+    return rec
+
+
+def _prfl(model_type, Fl, Hl, Wl, fp8=False, big=False):
+    from prfl_amd import block as B
+    from prfl_amd.train import PRFLTrainer
+    gen, lrm, qa, mlp = real_models(model_type, 2, 1)
+    for p in list(lrm.parameters()) + list(qa.parameters()) + list(mlp.parameters()):
+        p.requires_grad_(False)
+    if fp8:
+        gen.set_fp8_gemm(True, attn=True)
+        lrm.set_fp8_gemm(True, attn=True)
+    i2v = model_type == "i2v"
+    lat, text, clip, cond = inputs(Fl, Hl, Wl, i2v)
+    L = Fl * (Hl // 2) * (Wl // 2)
+    tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=1.0, feature_layer=(1,),
+                     optimizer_state_on_host=big)
+    params = tr.params
+    rec = fresh_grad_recorder(tr.reducer, params)
+    before = [p.detach().clone() for p in params[:8]] + [params[-1].detach().clone()]
+    cap = BlockCapture(gen.blocks[0])
+    if big:
+        B.set_attn_stash_budget(int(4e9))
+    try:
+        a = tr.sft_step(0, lat, text, L, image_embeds=clip, cond=cond)
+        b = tr.reward_step(0, lat, text, L, image_embeds=clip, cond=cond, mid_timestep=0)
+        tr.optimizer.wait()
+        torch.cuda.synchronize()
+    finally:
+        B.set_attn_stash_budget(0)
+    for out in (a, b):
+        assert torch.isfinite(torch.as_tensor(out["loss"])).all() and float(out["loss"]) > 0
+        gn = float(out["grad_norm"])
+        assert gn > 0 and gn == gn and gn != float("inf")
+    assert b.get("mid") == 0 and not b.get("skipped")
+    assert len(rec) == 2 and all(bad == 0 and zero == 0 for bad, zero in rec), rec
+    assert tr.optimizer.step_count == 2
+    moved = [not torch.equal(p0, p.detach()) for p0, p in zip(before, params[:8] + [params[-1]])]
+    assert all(moved), moved
+    rep = check_block_vs_oracle(cap, i2v=i2v, fp8=fp8)
+    rep.update(sft_loss=float(a["loss"]), rwd_loss=float(b["loss"]), reward=float(b["reward"]),
+               grad_norms=(float(a["grad_norm"]), float(b["grad_norm"])))
+    print(model_type, (Fl, Hl, Wl), "fp8" if fp8 else "bf16", rep)
+
+
+def test_c2_pavrm_t2v_480_real_width():
+    """C2 `train_pavrm_t2v_480`: PAVRMTrainer.step (BCE, three parameter groups, trunk clip) on a
+    real-width 2-block trunk + QueryAttention + MLP at 480p x 81f (L = 32 760), two steps."""
+    from prfl_amd.train import PAVRMTrainer
+    _, lrm, qa, mlp = real_models("t2v", 0, 2)
+    tr = PAVRMTrainer(lrm, qa, mlp, feature_layer=(2,))
+    params = tr.trunk_params + tr.head_params
+    rec = fresh_grad_recorder(tr.reducer, params)
+    lat, text, _, _ = inputs(21, 60, 104)
+    cap = BlockCapture(lrm.blocks[0])
+    before = [p.detach().clone() for p in params]
+    outs = []
+    for s, label in enumerate((1.0, 0.0)):
+        outs.append(tr.step(lat, text, 21 * 30 * 52, torch.tensor([label], device=DEV)))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.isfinite(torch.as_tensor(o["loss"])).all() and float(o["loss"]) > 0
+        p = float(o["prob"].flatten()[0])
+        assert 0 < p < 1
+        assert float(o["grad_norm"]) > 0
+    assert len(rec) == 2 and all(bad == 0 and zero == 0 for bad, zero in rec), rec
+    assert all(not torch.equal(b, p.detach()) for b, p in zip(before, params))
+    rep = check_block_vs_oracle(cap)
+    rep.update(losses=[float(o["loss"]) for o in outs], grad_norms=[float(o["grad_norm"]) for o in outs])
+    print("C2", rep)
+
+
+def test_c3_prfl_t2v_480_real_width():
+    """C3 `train_prfl_t2v_480`: one PRFL iteration (SFT step + reward step at mid_timestep 0)
+    with a real-width 2-block generator and 1-block reward trunk at 480p x 81f (L = 32 760)."""
+    _prfl("t2v", 21, 60, 104)
+
+
+def test_c4_prfl_t2v_720_real_width():
+    """C4 `train_prfl_t2v_720`: the same at 720p x 81f (L = 73 920), AdamW moments in pinned
+    host memory and the attention stash on (the 720p memory plan's code paths)."""
+    _prfl("t2v", 21, 88, 160, big=True)
+
+
+def test_c5_prfl_i2v_720_fp8_real_width():
+    """C5 `train_prfl_i2v_720`: the I2V model (36 input channels, 257 CLIP tokens of image
+    cross-attention) at 720p x 81f with the fp8 path on (set_fp8_gemm(True, attn=True))."""
+    _prfl("i2v", 21, 88, 160, fp8=True, big=True)

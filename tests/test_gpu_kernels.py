@@ -625,3 +625,40 @@ def test_colsum_reduce(ops, P, N):
     out2 = base.clone()
     ops.colsum_reduce(part, out=out2, accumulate=True)
     assert (out2.double() - (ref + base.double())).abs().max().item() <= 1e-4
+
+
+def test_adamw_zero_grad_in_step_is_bit_exact(ops):
+    """step(zero_grad=True) (the update kernel zeroes each gradient once read, buffers kept) ==
+    step() + zero_grad(): identical parameters over several steps with the next gradient
+    accumulated into the zeroed buffer, overlapped, with device and host-streamed moments; the
+    gradient tensors are the same storage throughout."""
+    from prfl_amd.optim import AdamW
+    g = torch.Generator().manual_seed(8)
+    shapes = [(3000,), (257, 33), (5,), (1024, 64)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(4)]
+    for host in (False, True):
+        a = [x.clone().to(DEV).requires_grad_(True) for x in base]
+        b = [x.clone().to(DEV).requires_grad_(True) for x in base]
+        oa = AdamW(a, lr=1e-2, state_on_host=host)
+        ob = AdamW(b, lr=1e-2, state_on_host=host, overlap=True, ring_slots=2)
+        ptrs = None
+        for gs in grads:
+            for pa, pb, gr in zip(a, b, gs):
+                pa.grad = gr.to(DEV)
+                if pb.grad is None:
+                    pb.grad = gr.to(DEV)
+                else:
+                    ob.wait([pb])
+                    pb.grad += gr.to(DEV)              # AccumulateGrad into the zeroed buffer
+            oa.step()
+            oa.zero_grad()
+            ob.step(zero_grad=True)
+            ob.wait()
+            assert all(bool((pb.grad == 0).all()) for pb in b)
+            p2 = [pb.grad.data_ptr() for pb in b]
+            assert ptrs is None or p2 == ptrs
+            ptrs = p2
+        ob.synchronize()
+        for pa, pb in zip(a, b):
+            assert torch.equal(pa, pb), host

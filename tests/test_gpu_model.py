@@ -344,11 +344,11 @@ def test_prfl_trainer_two_iterations_vs_reference(golden, fixture):
         end()
         rec["fresh"] = {n: p.grad - rec["before"][n] for n, p in named.items()}
 
-    def hook_step():
+    def hook_step(**kw):
         tr.optimizer.wait()
         rec["clipped"] = {n: p.grad.clone() for n, p in named.items()}
         rec["p0"] = {n: p.detach().clone() for n, p in named.items()}
-        ostep()
+        ostep(**kw)
         tr.optimizer.wait()
         rec["upd"] = {n: p.detach() - rec["p0"][n] for n, p in named.items()}
     tr.reducer.begin, tr.reducer.end, tr.optimizer.step = hook_begin, hook_end, hook_step
@@ -509,10 +509,10 @@ def test_toy_pavrm_steps_vs_reference(golden):
     def capture(opt, tag):          # grads as the optimizer sees them (after the trunk clip)
         f = opt.step
 
-        def step():
+        def step(**kw):
             grads[tag] = [p.grad.detach().clone() for p in opt.params]
             orig_step[tag] = [p.detach().clone() for p in opt.params]
-            f()
+            f(**kw)
         opt.step = step
     capture(tr.opt_trunk, "trunk")
     capture(tr.opt_head, "head")
