@@ -18,8 +18,8 @@ Each checks: finite losses and gradient norms; every trainable parameter's fresh
 and non-zero; the optimizer moved the parameters; and block 0's output during the step, on 1 024
 rows spread over the sequence, against the oracle run on the captured block inputs (keys and
 values from all L tokens): output <= 1e-2 and residual update <= 3e-2 rel-L2 (bf16 configs), and
-for C5 the update held to the fp32 truth within 16 x the bf16 oracle's own error (the rule of
-test_gpu_fp8.py::test_block_fp8_vs_fp32_truth) and 1e-1.
+for C5 the update and the output held to the fp32 truth within 16 x the bf16 oracle's own error
+(the rule of test_gpu_fp8.py::test_block_fp8_vs_fp32_truth) and 1e-1.
 """
 import pytest
 import torch
@@ -119,8 +119,13 @@ def check_block_vs_oracle(cap, i2v=False, fp8=False):
         t32 = oracle(True)
         rep["update vs truth"] = rel(out - xr, t32 - xr)
         rep["oracle bf16 update vs truth"] = rel(ref - xr, t32 - xr)
-        assert rep["update vs truth"] <= 16 * rep["oracle bf16 update vs truth"], rep
-        assert rep["update vs truth"] < 1e-1 and rep["out vs oracle"] < 1e-2, rep
+        rep["out vs truth"] = rel(out, t32)
+        rep["oracle bf16 out vs truth"] = rel(ref, t32)
+        # (at block 0 the update outweighs the patch-embedded residual, so the output carries the
+        # update's e4m3 error: both are held to the rule, not to the bf16 path's 1e-2)
+        for k in ("update", "out"):
+            assert rep[k + " vs truth"] <= 16 * rep["oracle bf16 %s vs truth" % k], rep
+            assert rep[k + " vs truth"] < 1e-1, rep
     else:
         assert rep["out vs oracle"] < 1e-2 and rep["update vs oracle"] < 3e-2, rep
     return rep
