@@ -677,6 +677,9 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 #ifndef GEMM4_BFIRST
 #define GEMM4_BFIRST 0
 #endif
+#ifndef GEMM4_PREWAIT
+#define GEMM4_PREWAIT 1
+#endif
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
@@ -784,6 +787,12 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   asm volatile("" ::: "memory");
   bf16x8 fa[8], fb[8], ga[8], gb[8];
   read(0, fa, fb);
+  // GEMM4_PREWAIT: retire every LDS / scalar load before the loop with a wait the compiler's
+  // waitcnt pass sees (the builtin, not asm): else a kernel-argument load still in flight from
+  // the preheader (scalar loads complete out of order) made the pass drain every LDS read
+  // (lgkmcnt(0)) before the first MFMA of every other slice, exposing the latency of the two
+  // reads issued right after the barrier
+  if (GEMM4_PREWAIT) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
   for (int j = 0; j < ns; j += 2) {
     step(j, fa, fb, ga, gb);
     step(j + 1, ga, gb, fa, fb);
