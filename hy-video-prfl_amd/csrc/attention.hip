@@ -535,10 +535,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #ifndef ATTN_BWD_NEGD
 #define ATTN_BWD_NEGD 1
 #endif
-// ATTN_DQ_PF: the dQ kernel's LDS fragment reads one MFMA step ahead (see there)
-#ifndef ATTN_DQ_PF
-#define ATTN_DQ_PF 0
-#endif
+// (A dQ variant with every LDS fragment read one MFMA step ahead -- the LSE start rebuilt by
+// v_mov to free the registers -- measured bit-identical and no faster: the partner wave already
+// covers the read latency; profiles/r04_attn_dq_pf_ab.txt)
 __global__ void attn_delta_kernel(const bf16* __restrict__ dO, int64_t lddo, int64_t bdo,
                                   const bf16* __restrict__ O, int64_t ldo, int64_t bo,
                                   float* __restrict__ delta, int B, int Lq, int H) {
@@ -803,7 +802,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // score; the tuple costs 16 VGPRs, paid for by packing dS one key sub-tile at a time
   f32x16 lset;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lset[r] = ATTN_DQ_PF ? 0.f : lse;
+  for (int r = 0; r < 16; ++r) lset[r] = lse;
   if (QS) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = -qf[ks];
@@ -862,44 +861,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
       const int row = kt * 32 + l32;
-      if (ATTN_DQ_PF) {
-        // the K / V row fragments of step ks+1 are read before the MFMAs of step ks (one step
-        // of read-ahead, pinned by sched_group_barrier); the LSE start of the S accumulators is
-        // rebuilt per sub-tile by 16 v_mov instead of a loop-invariant 16-VGPR tuple, which pays
-        // for the read-ahead registers
-        if (QS) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) asm volatile("v_mov_b32 %0, %1" : "=v"(st[r]) : "v"(lse));
-        }
-        bf16x8 kc = *(const bf16x8*)(Ks + offB(row, hh * 16));
-        bf16x8 vc = *(const bf16x8*)(Vs + off16(row, hh));
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          bf16x8 kn = kc, vn = vc;
-          if (ks < 7) {
-            kn = *(const bf16x8*)(Ks + offB(row, ((ks + 1) * 2 + hh) * 16));
-            vn = *(const bf16x8*)(Vs + off16(row, (ks + 1) * 2 + hh));
-          }
-          st = mfma32(kc, qf[ks], st);
-          dpt = mfma32(vc, df[ks], dpt);
-          kc = kn;
-          vc = vn;
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-        for (int ks = 0; ks < 7; ++ks) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      } else {
       st = mfma32(*(const bf16x8*)(Ks + offB(row, hh * 16)), qf[0], QS ? lset : st);
       dpt = mfma32(*(const bf16x8*)(Vs + off16(row, hh)), df[0], dpt);
 #pragma unroll
       for (int ks = 1; ks < 8; ++ks) {
         st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
         dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
-      }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -919,28 +886,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                            f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
       if (ATTN_BWD_DMA_MID && kt == 0 && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
       // dQ^T += K^T dS^T for this key sub-tile (per dQ tile the same (kt, s2) summation order)
-      if (ATTN_DQ_PF) {          // transposed K reads one MFMA ahead
-        auto ktr = [&](int i) {
-          const int dt = i >> 1, s2 = i & 1;
-          const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-          const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          return cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
-        };
-        bf16x8 kc = ktr(0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bf16x8 kn = i < 7 ? ktr(i + 1) : kc;
-          dq[i >> 1] = mfma32(kc, dsp[i & 1], dq[i >> 1]);
-          kc = kn;
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-      } else {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
@@ -950,7 +895,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
           const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
           dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
         }
-      }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

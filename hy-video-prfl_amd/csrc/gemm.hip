@@ -670,13 +670,6 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
   }
 }
 
-// GEMM4_BFIRST: read the next slice's 8 B fragments in chunks 0-3 and its A fragments in
-// chunks 4-7 (fragment i two chunks before... chunk i of the next slice needs A fragment i and
-// ALL B fragments): with the interleaved order the last B fragment lands one chunk before the
-// next slice's first MFMA, and the waitcnt pass drained every LDS read (lgkmcnt(0)) there
-#ifndef GEMM4_BFIRST
-#define GEMM4_BFIRST 0
-#endif
 #ifndef GEMM4_PREWAIT
 #define GEMM4_PREWAIT 1
 #endif
@@ -736,16 +729,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   };
   auto read = [&](int j, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
     const char* st = smem + (j & 3) * SLICE4;
-    if (GEMM4_BFIRST) {     // the loop's read order (below): the waitcnt state at the loop head
-#pragma unroll             // is the same from the preheader and from the back edge
-      for (int i = 0; i < 8; ++i) bf[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
-    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) af[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
-    if (!GEMM4_BFIRST) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) bf[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
-    }
+    for (int i = 0; i < 8; ++i) bf[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
   };
   auto step = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8]) {
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own part of slice j+1 landed
@@ -760,16 +747,8 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       piece(i, jd, sd);
-      if (!GEMM4_BFIRST) {
-        na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
-        nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
-      } else if (i < 4) {   // all of slice j+1's B fragments in the first half (its chunk 0
-        nb[2 * i] = read_frag4<B_KC>(st + HALF4, wn * 128 + 2 * i * 16, lane);   // needs all 8),
-        nb[2 * i + 1] = read_frag4<B_KC>(st + HALF4, wn * 128 + (2 * i + 1) * 16, lane);
-      } else {              // A fragment i in chunk 4 + i / 2 (chunk i of slice j+1 needs it)
-        na[2 * i - 8] = read_frag4<A_KC>(st, wm * 128 + (2 * i - 8) * 16, lane);
-        na[2 * i - 7] = read_frag4<A_KC>(st, wm * 128 + (2 * i - 7) * 16, lane);
-      }
+      na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
+      nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj)   // AGPR accumulators: the MFMA as inline asm ("+a") keeps
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"   // hipcc from switching them to
@@ -790,8 +769,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // GEMM4_PREWAIT: retire every LDS / scalar load before the loop with a wait the compiler's
   // waitcnt pass sees (the builtin, not asm): else a kernel-argument load still in flight from
   // the preheader (scalar loads complete out of order) made the pass drain every LDS read
-  // (lgkmcnt(0)) before the first MFMA of every other slice, exposing the latency of the two
-  // reads issued right after the barrier
+  // (lgkmcnt(0)) before the first MFMA of every other slice.  Measured neutral (+-0.5 %,
+  // bit-identical: profiles/r04_gemm_lgkm_ab.txt) -- that drain was not a stall; kept as the
+  // cleaner loop
   if (GEMM4_PREWAIT) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
   for (int j = 0; j < ns; j += 2) {
     step(j, fa, fb, ga, gb);

@@ -306,9 +306,12 @@ def test_attn_fp8_masked_keys_set_no_scale(Lq, Lk, klen):
     H = 2
     g = torch.Generator(device=DEV).manual_seed(Lk + klen)
     C = H * 128
-    q = torch.randn(Lq, C, generator=g, device=DEV).to(torch.bfloat16)
-    k = torch.randn(Lk, C, generator=g, device=DEV).to(torch.bfloat16)
-    v = torch.randn(Lk, C, generator=g, device=DEV).to(torch.bfloat16)
+    # operands as test_attn_fp8_vs_dequantised_fp64 draws them (its 2.5e-2 bound is the e4m3
+    # rounding of P for that score spread)
+    q = (torch.randn(Lq, C, generator=g, device=DEV) * 1.5).to(torch.bfloat16)
+    k = (torch.randn(Lk, C, generator=g, device=DEV) * 1.5).to(torch.bfloat16)
+    v = torch.randn(Lk, C, generator=g, device=DEV)
+    v = (v * torch.linspace(0.1, 3.0, C, device=DEV)).to(torch.bfloat16)
     k0, v0 = k.clone(), v.clone()
     k0[klen:] = 0
     v0[klen:] = 0
