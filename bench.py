@@ -301,12 +301,12 @@ def main():
         # (bit-identical to recomputing them; block.py): the budget bounds the bytes kept at any
         # time.  T2V: 38 GB keeps all 40 generator blocks + the 8 reward-model blocks at 720p
         # (0.77 GB each), so no grad-enabled L x L attention forward is recomputed; 20 GB when
-        # RCCL's buffers sit beside it (N > 1).  I2V (16.4 B parameters): 22 GB at N = 1, none at
-        # N > 1.
+        # RCCL's buffers sit beside it (N > 1).  I2V (16.4 B parameters, 66 GB of fp32 gradients
+        # resident through the iteration): 10 GB at N = 1, none at N > 1.
         from prfl_amd import block as _blk
         default_gb = "0"
         if big_fits(args):
-            default_gb = ("22" if world == 1 else "0") if i2v else ("38" if world == 1 else "20")
+            default_gb = ("10" if world == 1 else "0") if i2v else ("38" if world == 1 else "20")
         if args.toy:
             default_gb = "0.001"
         stash_gb = float(os.environ.get("PRFL_ATTN_STASH_GB", default_gb))
@@ -469,6 +469,9 @@ def main():
         "config": {"workload": workload, "model": model, "latent": [16, Fl, Hl, Wl],
                    "seq_len": L, "global_batch": world, "parallelism": f"dp{world}"},
         "peak_hbm_gb": round(peak_res, 1), "peak_alloc_gb_rank0": round(peak_alloc, 1),
+        # fp32 gradients stay allocated across iterations (AdamW.step(zero_grad=True)): the peak
+        # is that of every iteration, accumulating or not
+        "grad_buffers": "persistent",
         "stash_gb": stash_gb,
         "algorithmic_tflop_per_step": round(flops_it / 1e12, 1),
         "achieved_tflops_per_gpu": round(flops_it * steps / dt / 1e12, 1),

@@ -7,7 +7,7 @@ Two estimates, both per GPU:
   * analytic: the resident tensors of DESIGN.md §2 plus the reward step's peak working set;
   * from measurement: an N = 1 bench's peak allocated / reserved (profiles/r0*_bench_*.json),
     minus the stash the N = 1 run kept, plus the N > 1 stash and RCCL's buffers.
-What differs at N > 1 (bench.py): the attention-output stash budget (T2V 38 -> 20 GB, I2V 22 -> 0
+What differs at N > 1 (bench.py): the attention-output stash budget (T2V 38 -> 20 GB, I2V 10 -> 0
 GB per step), the RCCL communicator buffers (estimate below), and the ZeRO-1 optimizer (the AdamW
 moments stay in pinned host memory; each rank streams 1/N of them through the same 3-slot HBM
 ring).  Every rank otherwise holds the same replica as the single-GPU run.
@@ -24,7 +24,7 @@ BLOCK = {"t2v": 351.4e6,                                   # per Wan
 P_GEN = {"t2v": 14.288e9, "i2v": 16.4e9}                   # bench.py / SURVEY §8
 P_HEAD = 3 * C * C + 4 * C + C * 1024 + 1024 * 512 + 512 + 1 + 1024 + 512   # QA + MLP
 STASH_PER_BLOCK = (L * C * 2 + NH * L * 4) / GB      # kept self-attention output + LSE
-STASH_DEFAULT = {("t2v", 1): 38.0, ("t2v", 8): 20.0, ("i2v", 1): 22.0, ("i2v", 8): 0.0}
+STASH_DEFAULT = {("t2v", 1): 38.0, ("t2v", 8): 20.0, ("i2v", 1): 10.0, ("i2v", 8): 0.0}
 
 
 def rccl_buffers_gb(world, channels=32, buff_bytes=4 << 20):
@@ -59,10 +59,17 @@ def analytic(world, stash_gb, model="t2v"):
 
 
 def from_measurement(world, stash_gb, path):
+    """(allocated, reserved) GB per rank at N = `world` from an N = 1 bench line.  Lines from
+    before round 4 (no "grad_buffers": "persistent") timed optimizer-boundary iterations whose
+    gradients were freed after the SFT step's update, so their peak lacks the fp32 gradients an
+    accumulating iteration (4 of every 5 at gradient_accumulation_steps 5) holds: added here."""
     d = json.load(open(path))
     alloc, res = d["peak_alloc_gb_rank0"], d["peak_hbm_gb"]
     kept = min(d.get("stash_gb", 38.0), (NL + 8) * STASH_PER_BLOCK)
     delta = min(stash_gb, (NL + 8) * STASH_PER_BLOCK) - kept + rccl_buffers_gb(world)
+    if d.get("grad_buffers") != "persistent":
+        model = "i2v" if "I2V" in d.get("config", {}).get("model", "") else "t2v"
+        delta += P_GEN[model] * 4 / GB
     return alloc + delta, res + delta
 
 
