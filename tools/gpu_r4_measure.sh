@@ -22,6 +22,8 @@ fi
 if [ "${SKIP_DISC:-0}" != "1" ]; then
   step pmc_disc 700 bash tools/pmc_bench_discriminate.sh $tag || exit $?
 fi
-step bench_pavrm480 300 python bench.py --workload pavrm_t2v_480 --steps 5 --warmup 1 || exit $?
-step bench_prfl480 420 python bench.py --workload prfl_t2v_480 --steps 2 --warmup 1 || exit $?
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
+  step bench_pavrm480 300 python bench.py --workload pavrm_t2v_480 --steps 5 --warmup 1 || exit $?
+  step bench_prfl480 420 python bench.py --workload prfl_t2v_480 --steps 2 --warmup 1 || exit $?
+fi
 echo session done
