@@ -130,6 +130,28 @@ __device__ __forceinline__ void xcd_tile(int ntile, int nbh, int& bh, int& tile,
   }
 }
 
+// (sample, head, tile) of a backward unit: the plain order (tile fastest, then head, then
+// sample) or, with XCD = 1, xcd_tile's XCD-aware grouping (the forward's mapping)
+template <bool XCD>
+__device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int& b, int& h, int& t) {
+  if (XCD) {
+    int bh;
+    xcd_tile(ntile, B * H, bh, t, unit);
+    b = bh / H;
+    h = bh % H;
+  } else {
+    b = unit / (ntile * H);
+    h = (unit / ntile) % H;
+    t = unit % ntile;
+  }
+}
+#ifndef ATTN_BWD_XCD_KV
+#define ATTN_BWD_XCD_KV 0
+#endif
+#ifndef ATTN_BWD_XCD_Q
+#define ATTN_BWD_XCD_Q 0
+#endif
+
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -576,7 +598,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   bool part;
   tail_unit(a.nmain_k, a.split_k, unit, share, part);
   const int nkt = (a.Lk + 255) / 256;
-  const int b = unit / (nkt * a.H), h = (unit / nkt) % a.H, k0 = (unit % nkt) * 256;
+  int b, h, kt0;
+  bwd_unit<ATTN_BWD_XCD_KV>(unit, nkt, a.H, a.B, b, h, kt0);
+  const int k0 = kt0 * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
@@ -779,7 +803,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   bool part;
   tail_unit(a.nmain_q, a.split_q, unit, share, part);
   const int nqt = (a.Lq + 255) / 256;
-  const int b = unit / (nqt * a.H), h = (unit / nqt) % a.H, q0 = (unit % nqt) * 256;
+  int b, h, qt0;
+  bwd_unit<ATTN_BWD_XCD_Q>(unit, nqt, a.H, a.B, b, h, qt0);
+  const int q0 = qt0 * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
@@ -963,7 +989,9 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
 // dV_s; dQ = scale * sum_s dQ_s.
 __global__ __launch_bounds__(256) void attn_merge_kv_kernel(AttnBwdArgs a) {
   const int unit = a.nmain_k + blockIdx.x, nkt = (a.Lk + 255) / 256;
-  const int b = unit / (nkt * a.H), h = (unit / nkt) % a.H, k0 = (unit % nkt) * 256;
+  int b, h, kt0;
+  bwd_unit<ATTN_BWD_XCD_KV>(unit, nkt, a.H, a.B, b, h, kt0);
+  const int k0 = kt0 * 256;
   const int c = (threadIdx.x & 31) * 4, r0 = blockIdx.y * 32;
   for (int row = r0 + (threadIdx.x >> 5); row < r0 + 32; row += 8) {
     const int key = k0 + row;
@@ -988,7 +1016,9 @@ __global__ __launch_bounds__(256) void attn_merge_kv_kernel(AttnBwdArgs a) {
 
 __global__ __launch_bounds__(256) void attn_merge_q_kernel(AttnBwdArgs a) {
   const int unit = a.nmain_q + blockIdx.x, nqt = (a.Lq + 255) / 256;
-  const int b = unit / (nqt * a.H), h = (unit / nqt) % a.H, q0 = (unit % nqt) * 256;
+  int b, h, qt0;
+  bwd_unit<ATTN_BWD_XCD_Q>(unit, nqt, a.H, a.B, b, h, qt0);
+  const int q0 = qt0 * 256;
   const int c = (threadIdx.x & 31) * 4, r0 = blockIdx.y * 32;
   for (int row = r0 + (threadIdx.x >> 5); row < r0 + 32; row += 8) {
     const int qo = q0 + row;
