@@ -151,6 +151,10 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
 #ifndef ATTN_BWD_XCD_Q
 #define ATTN_BWD_XCD_Q 0
 #endif
+// dQ kernel K / V ring depth: 2 (tile t+1 issued during tile t) or 3 (tile t+2: 144 KiB of LDS)
+#ifndef ATTN_DQ_STAGES
+#define ATTN_DQ_STAGES 2
+#endif
 
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -798,7 +802,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
 template <int NKT, bool QS>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];  // 2 stages of [K (image B) | V]
+  constexpr int NST = ATTN_DQ_STAGES;                        // ring stages of [K (image B) | V]
+  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
   int unit, share;
   bool part;
   tail_unit(a.nmain_q, a.split_q, unit, share, part);
@@ -828,7 +833,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // score; the tuple costs 16 VGPRs, paid for by packing dS one key sub-tile at a time
   f32x16 lset;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lset[r] = lse;
+  for (int r = 0; r < 16; ++r) lset[r] = ATTN_DQ_STAGES == 3 ? 0.f : lse;
   if (QS) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = -qf[ks];
@@ -871,15 +876,25 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     }
   };
   if (nkv > 0) dma(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
+  if (NST == 3) {          // tile 1 in flight across the first barrier: wait for tile 0 only
+    if (nkv > 1) dma(1, 1);
+    if (nkv > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
+  }
   __syncthreads();
   for (int t = 0; t < nkv; ++t) {
     const int kb = (t0 + t) * TK;
     // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it);
     // ATTN_BWD_DMA_MID: issued after the first key sub-tile's VALU block instead (LDS-DMA issue
     // costs less there than beside MFMAs and LDS reads)
-    if (!ATTN_BWD_DMA_MID && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
-    const char* Ks = smem + (t & 1) * SB;
+    // NST 3: tile t+2 into the stage tile t-1 used (every wave is past the barrier that ended
+    // tile t-1), so a tile's DMA has two tiles of compute to land instead of one
+    const int tn = NST == 3 ? t + 2 : t + 1;
+    const int stn = NST == 3 ? tn % 3 : (tn & 1);
+    if (!ATTN_BWD_DMA_MID && tn < nkv) dma(tn, stn);
+    const char* Ks = smem + (NST == 3 ? t % 3 : (t & 1)) * SB;
     const char* Vs = Ks + SV;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -887,7 +902,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
       const int row = kt * 32 + l32;
-      st = mfma32(*(const bf16x8*)(Ks + offB(row, hh * 16)), qf[0], QS ? lset : st);
+      if (QS && ATTN_DQ_STAGES == 3) {   // the LSE start rebuilt per sub-tile (16 v_mov): the
+#pragma unroll                            // loop-invariant 16-VGPR tuple would push the 3-stage
+        for (int r = 0; r < 16; ++r)      // ring's bookkeeping into scratch
+          asm volatile("v_mov_b32 %0, %1" : "=v"(st[r]) : "v"(lse));
+      }
+      st = mfma32(*(const bf16x8*)(Ks + offB(row, hh * 16)), qf[0],
+                  QS ? (ATTN_DQ_STAGES == 3 ? st : lset) : st);
       dpt = mfma32(*(const bf16x8*)(Vs + off16(row, hh)), df[0], dpt);
 #pragma unroll
       for (int ks = 1; ks < 8; ++ks) {
@@ -910,7 +931,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         dsp[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
                            f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
                            f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-      if (ATTN_BWD_DMA_MID && kt == 0 && t + 1 < nkv) dma(t + 1, (t + 1) & 1);
+      if (ATTN_BWD_DMA_MID && kt == 0 && tn < nkv) dma(tn, stn);
       // dQ^T += K^T dS^T for this key sub-tile (per dQ tile the same (kt, s2) summation order)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -923,7 +944,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NST == 3 && tn < nkv)     // tile t+1 landed; tile t+2's pieces may stay in flight
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }

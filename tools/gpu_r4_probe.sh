@@ -6,8 +6,8 @@ tag=${1:?tag}
 out=$GRAFT_REPO_ROOT/gpurun_out/$tag
 mkdir -p $out
 cd $GRAFT_REPO_ROOT/tools
-timeout -k 10 300 python ab_attn_libs.py ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_axboth.so \
-  ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_axboth.so --bwd --qs 0,1,2,3,4,5,6,7 --reps 4 \
+timeout -k 10 300 python ab_attn_libs.py ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_aq3.so ../ab/lib_axq3.so \
+  ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_aq3.so ../ab/lib_axq3.so --bwd --qs 0,1,2,3,4,5,6,7,8,9 --reps 4 \
   > $out/ab_bwd_xcd.log 2>&1
 rc=$?; echo "ab rc=$rc"; tail -3 $out/ab_bwd_xcd.log
 [ $rc -ne 0 ] && exit $rc
