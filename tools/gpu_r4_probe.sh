@@ -5,6 +5,10 @@
 tag=${1:?tag}
 out=$GRAFT_REPO_ROOT/gpurun_out/$tag
 mkdir -p $out
+cd $GRAFT_REPO_ROOT
+timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 $out/smoke.log
+[ $rc -ne 0 ] && exit $rc
 cd $GRAFT_REPO_ROOT/tools
 timeout -k 10 300 python ab_attn_libs.py ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_aq3.so ../ab/lib_axq3.so \
   ../ab/lib_abase.so ../ab/lib_axq.so ../ab/lib_axkv.so ../ab/lib_aq3.so ../ab/lib_axq3.so --bwd --qs 0,1,2,3,4,5,6,7,8,9 --reps 4 \
