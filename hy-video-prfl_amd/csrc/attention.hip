@@ -155,6 +155,16 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
 #ifndef ATTN_DQ_STAGES
 #define ATTN_DQ_STAGES 2
 #endif
+// dQ kernel wave stagger (needs the 3-stage ring): waves 4-7 run one barrier (= one key tile)
+// behind waves 0-3 at s_setprio 1, so on each SIMD one wave's MFMA-dense opening overlaps its
+// partner's exp / dS packing instead of both issuing the same phase together (MI355X guide,
+// two waves per SIMD, items 4 and 9).  Waves 0-3 issue their pieces of tile t+1 during tile t,
+// waves 4-7 theirs of tile t+2 during their tile t (= the leaders' t+1): both land before the
+// barrier the leaders pass to read it, and the stage they fill was last read by either half
+// before the barrier that opened the issuing window (the forward's ring discipline)
+#ifndef ATTN_DQ_STAGGER
+#define ATTN_DQ_STAGGER 0
+#endif
 
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -218,8 +228,16 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
+// VT (self-attention forward, prfl_attn_fwd_l2q_vt_ws): V arrives in the key-chunked transposed
+// layout of prfl_attn_v_to_vt -- per (sample, head) [Lkp/8 chunks][128 d][8 keys], the 8 keys of
+// chunk 2j + h being 16j + 4h + {0,1,2,3,8,9,10,11} (the P^T fragment's k-slot order), zero from
+// Lk up to Lkp = Lk rounded up to 96.  A 96-key tile is then one contiguous 24 KiB run whose LDS
+// image [chunk][d] serves every V^T fragment as ONE conflict-free ds_read_b128 (32 lanes = 32 d
+// rows of one chunk) instead of two ds_read_b64_tr_b16 on the row-major image: half the LDS
+// read instructions of the P.V product, the same operand values in the same k-slot order
+// (outputs bit-identical to the row-major path)
 
-template <bool SHORT_KV, int SCHED, int NKT, bool QS>
+template <bool SHORT_KV, int SCHED, int NKT, bool QS, bool VT = false>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
@@ -247,7 +265,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const bf16* Qb = a.Q + b * a.bq + h * HD;
   const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
+  static_assert(!VT || (NKT == 3 && !SHORT_KV), "VT: 96-key tiles of the long-KV forward");
+  const bf16* Vb = VT ? a.V + (int64_t)bh * a.bv : a.V + b * a.bv + h * HD;   // VT: bv = Lkp*128
 
   bf16x8 qf[8];
   {
@@ -281,9 +300,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) koff[ks] = off16(l32, ks * 2 + hh);   // + kt*32 rows
   // (rows r and r + 8 of a transposed read carry different swizzles; + 16 s2 + 32 kt rows keep them)
-  int voff[4], voff8[4];
+  int voff[4], voff8[4], vtoff[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
+    vtoff[dt] = hh * 2048 + (dt * 32 + l32) * 16;     // VT image: chunk 2 (2kt + s2) + hh, row d
     voff[dt] = SV + offB(4 * (g >> 1) + qq, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
     voff8[dt] = SV + offB(4 * (g >> 1) + qq + 8, (dt * 32 + 16 * (g & 1) + 4 * pp) * 2);
   }
@@ -297,7 +317,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     const int row = (w * NKT + i) * 4 + (lane >> 4), pc = lane & 15;
     const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
     vok[i] = (uint32_t)(row * a.ldk * 2) + ((pc ^ (row & 15)) << 4);
-    vov[i] = (uint32_t)(row * a.ldv * 2) + ((pc ^ swzb) << 4);
+    vov[i] = VT ? (uint32_t)((w * NKT + i) * 1024 + lane * 16)       // contiguous, lane-linear
+                : (uint32_t)(row * a.ldv * 2) + ((pc ^ swzb) << 4);
   }
   auto dma = [&](int t, int st) {      // local tile t = key tile t0 + t
     char* Ks = smem + st * SB;
@@ -305,7 +326,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     const int tg = t0 + t;
     const int rows = min(a.Lk - tg * TK, TK);
     const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
-    const i32x4 sv = make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
+    const i32x4 sv = VT ? make_srd(Vb + (int64_t)tg * TK * HD, (uint32_t)SV)
+                        : make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
 #pragma unroll
     for (int i = 0; i < NKT; ++i) {
       dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
@@ -361,7 +383,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
             const int ro = (kt * 32 + 16 * s2) * 256;
-            const bf16x8 vf = cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
+            const bf16x8 vf = VT ? *(const bf16x8*)(Vs + SV + (kt * 4 + 2 * s2) * 2048 + vtoff[dt])
+                                 : cat8(lds_read_tr(Vs + voff[dt] + ro), lds_read_tr(Vs + voff8[dt] + ro));
             o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
           }
       }
@@ -875,8 +898,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                 lds_addr(Vs + (w * NKT + i) * 1024));
     }
   };
+  static_assert(!ATTN_DQ_STAGGER || NST == 3, "the dQ stagger needs the 3-stage ring");
+  const bool lag = ATTN_DQ_STAGGER && w >= 4;
   if (nkv > 0) dma(0, 0);
-  if (NST == 3) {          // tile 1 in flight across the first barrier: wait for tile 0 only
+  if (ATTN_DQ_STAGGER) {   // waves 4-7 also own their pieces of tile 1 (issued 2 ahead)
+    if (lag && nkv > 1) dma(1, 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  } else if (NST == 3) {   // tile 1 in flight across the first barrier: wait for tile 0 only
     if (nkv > 1) dma(1, 1);
     if (nkv > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");
     else __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -884,6 +912,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): Q / dO fragments, tile 0
   }
   __syncthreads();
+  if (lag) {               // the lagging half: one barrier behind, static priority 1
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
   for (int t = 0; t < nkv; ++t) {
     const int kb = (t0 + t) * TK;
     // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it);
@@ -891,7 +924,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     // costs less there than beside MFMAs and LDS reads)
     // NST 3: tile t+2 into the stage tile t-1 used (every wave is past the barrier that ended
     // tile t-1), so a tile's DMA has two tiles of compute to land instead of one
-    const int tn = NST == 3 ? t + 2 : t + 1;
+    const int tn = ATTN_DQ_STAGGER ? (lag ? t + 2 : t + 1) : NST == 3 ? t + 2 : t + 1;
     const int stn = NST == 3 ? tn % 3 : (tn & 1);
     if (!ATTN_BWD_DMA_MID && tn < nkv) dma(tn, stn);
     const char* Ks = smem + (NST == 3 ? t % 3 : (t & 1)) * SB;
@@ -944,10 +977,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         }
       }
     }
-    if (NST == 3 && tn < nkv)     // tile t+1 landed; tile t+2's pieces may stay in flight
+    if (!ATTN_DQ_STAGGER && NST == 3 && tn < nkv)   // tile t+1 landed; t+2 may stay in flight
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (ATTN_DQ_STAGGER && !lag) {   // the leaders' extra barrier: the same count on every wave
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
@@ -1510,6 +1547,39 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_lp_kernel(AttnF8Args f) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// V [B][Lk][H*128] (row stride ldv, sample stride bv) -> the VT layout of the long-KV forward
+// (see VT at attn_fwd_kernel): one workgroup per (sample, head, 64-key group); the 64 x 128 block
+// is read as coalesced 16-B row pieces into LDS, each thread then writes two 16-B chunks (the
+// eight keys 16j + 4h + {0,1,2,3,8,9,10,11} of one d), every output run contiguous; keys >= Lk
+// are written as zeros up to Lkp
+__global__ __launch_bounds__(256) void attn_v_to_vt_kernel(const bf16* __restrict__ V, int64_t ldv,
+                                                          int64_t bv, bf16* __restrict__ VT,
+                                                          int Lk, int Lkp, int H) {
+  __shared__ bf16 t[64][HD + 8];                     // +8: rows 16 B apart mod the bank window
+  const int grp = blockIdx.x, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+  const int k0 = grp * 64;
+  const bf16* Vb = V + b * bv + h * HD;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {                      // 64 rows x 16 pieces of 8 d
+    const int r = i * 16 + (tid >> 4), pc = tid & 15, key = k0 + r;
+    bf16x8 x = {};
+    if (key < Lk) x = *(const bf16x8*)(Vb + (int64_t)key * ldv + pc * 8);
+    *(bf16x8*)&t[r][pc * 8] = x;
+  }
+  __syncthreads();
+  bf16* out = VT + ((int64_t)b * H + h) * Lkp * HD + (int64_t)k0 * HD;
+  const int d = tid & 127, c0 = tid >> 7;            // chunks c0, c0 + 2, ... of the 8 in 64 keys
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = c0 + 2 * i, j = c >> 1, hb = c & 1, kb = 16 * j + 4 * hb;
+    if (k0 + 8 * c >= Lkp) break;
+    const bf16x8 y = {t[kb][d], t[kb + 1][d], t[kb + 2][d], t[kb + 3][d],
+                      t[kb + 8][d], t[kb + 9][d], t[kb + 10][d], t[kb + 11][d]};
+    *(bf16x8*)(out + ((int64_t)c * HD + d) * 8) = y;
+  }
+}
+int64_t vt_keys(int64_t Lk) { return (Lk + 95) / 96 * 96; }
+
 // Split-KV tail of the long-KV forward.  One workgroup per CU (144 KiB of LDS), so the grid
 // runs in rounds of #CU; when the last round is at most half full and every unit has many key
 // tiles, each of its `rem` units is split over `split` = #CU / rem (<= 8) workgroups: the final
@@ -1576,9 +1646,15 @@ namespace {
 int attn_fwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk, int64_t bk,
                   const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo, int64_t bo,
                   float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len,
-                  float scale, bool l2q, void* ws, int64_t ws_bytes, void* stream) {
+                  float scale, bool l2q, void* ws, int64_t ws_bytes, void* stream,
+                  bool vt = false) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  if (vt && (!l2q || Lk < 4096)) return (int)hipErrorInvalidValue;   // long-KV kernel only
+  if (vt) {
+    ldv = 0;
+    bv = vt_keys(Lk) * HD;                      // per (sample, head) run of the VT layout
+  }
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(ws) ||
       (ldq | ldk | ldv | ldo) % 8)
     return (int)hipErrorInvalidValue;
@@ -1603,7 +1679,9 @@ int attn_fwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
   if (kid == KID_ATTN_FWD) a.clk = prfl_prof::clk_slot();
   const dim3 grid((unsigned)(nmain + rem * split));
   if (kid == KID_ATTN_FWD) {
-    if (l2q)
+    if (vt)
+      hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, true, true>), grid, dim3(512), 0, s, a);
+    else if (l2q)
       hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, true>), grid, dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, false>), grid, dim3(512), 0, s, a);
@@ -1640,6 +1718,40 @@ extern "C" int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, cons
                                     int64_t ws_bytes, void* stream) {
   return attn_fwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, lse2, B, Lq, Lk, H, k_len,
                        1.f, true, ws, ws_bytes, stream);
+}
+
+// V -> the VT layout (see attn_fwd_kernel): vt holds prfl_attn_vt_bytes(B, Lk, H) bytes
+extern "C" int64_t prfl_attn_vt_bytes(int64_t B, int64_t Lk, int64_t H) {
+  if (B <= 0 || Lk <= 0 || H <= 0) return 0;
+  return B * H * vt_keys(Lk) * HD * 2;
+}
+
+extern "C" int prfl_attn_v_to_vt(const void* v, int64_t ldv, int64_t bv, void* vt, int64_t B,
+                                 int64_t Lk, int64_t H, void* stream) {
+  if (B <= 0 || Lk <= 0 || H <= 0) return 0;
+  if (!aligned16(v) || !aligned16(vt) || ldv % 8 || bv % 8 || Lk > 0x7fffffff || H > 65535 ||
+      B > 65535)
+    return (int)hipErrorInvalidValue;
+  const int64_t lkp = vt_keys(Lk);
+  hipStream_t s = (hipStream_t)stream;
+  prfl_prof::begin(KID_ELTWISE, s);
+  hipLaunchKernelGGL(attn_v_to_vt_kernel, dim3((unsigned)((lkp + 63) / 64), (unsigned)H, (unsigned)B),
+                     dim3(256), 0, s, (const bf16*)v, ldv, bv, (bf16*)vt, (int)Lk, (int)lkp, (int)H);
+  prfl_prof::set_work(4.0 * B * H * HD * (double)lkp);
+  prfl_prof::end(KID_ELTWISE, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+// prfl_attn_fwd_l2q_ws with V in the VT layout (prfl_attn_v_to_vt; long KV, Lk >= 4096, only):
+// outputs bit-identical to prfl_attn_fwd_l2q_ws on the row-major V
+extern "C" int prfl_attn_fwd_l2q_vt_ws(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                       int64_t ldk, int64_t bk, const void* vt, void* o, int64_t ldo,
+                                       int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk,
+                                       int64_t H, int64_t k_len, void* ws, int64_t ws_bytes,
+                                       void* stream) {
+  return attn_fwd_impl(q, ldq, bq, k, ldk, bk, vt, 0, 0, o, ldo, bo, lse2, B, Lq, Lk, H, k_len,
+                       1.f, true, ws, ws_bytes, stream, true);
 }
 
 extern "C" int prfl_attn_fwd(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,

@@ -28,6 +28,10 @@ SIGNATURES = {
     "prfl_attn_fwd_ws_bytes": [I64, I64, I64, I64, I64],
     "prfl_attn_fwd_l2q_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
                              I64, I64, P, I64, P],
+    "prfl_attn_vt_bytes": [I64, I64, I64],
+    "prfl_attn_v_to_vt": [P, I64, I64, P, I64, I64, I64, P],
+    "prfl_attn_fwd_l2q_vt_ws": [P, I64, I64, P, I64, I64, P, P, I64, I64, P, I64, I64, I64, I64, I64,
+                                P, I64, P],
     "prfl_attn_fwd_fp8": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I64,
                           I64, I64, F32, P, I64, P],
     "prfl_attn_fwd_fp8_ws_bytes": [I64, I64, I64, I64, I64],
@@ -75,7 +79,7 @@ SIGNATURES = {
 }
 
 # entries that return a value other than a hipError_t code
-RESTYPES = {"prfl_attn_fwd_ws_bytes": I64, "prfl_attn_fwd_fp8_ws_bytes": I64, "prfl_attn_bwd_ws_bytes": I64}
+RESTYPES = {"prfl_attn_fwd_ws_bytes": I64, "prfl_attn_vt_bytes": I64, "prfl_attn_fwd_fp8_ws_bytes": I64, "prfl_attn_bwd_ws_bytes": I64}
 
 # kernel ids of the profiling hooks (csrc/common.h)
 KID = dict(gemm=0, attn_fwd=1, attn_fwd_short=2, attn_bwd_dkdv=3, attn_bwd_dq=4, ln=5, rms=6,

@@ -213,10 +213,17 @@ def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_s
     return dx, colsum_reduce(p0)
 
 
+# the long-KV q_log2 forward reads V from its key-chunked transposed image (prfl_attn_v_to_vt +
+# prfl_attn_fwd_l2q_vt_ws: one ds_read_b128 per V^T fragment; outputs bit-identical)
+ATTN_VT = True
+VT_MIN_KEYS = 4096
+
+
 def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None, q_log2=False):
     """q [Lq, H*128], k/v [Lk, H*128] (row-strided views) -> (o bf16 [Lq, H*128], lse2 [H, Lq]).
     q_log2: q is already multiplied by softmax_scale * log2(e) (rms_rope_fwd out_scale=L2Q_SCALE);
-    scale is then unused (prfl_attn_fwd_l2q_ws)."""
+    scale is then unused (prfl_attn_fwd_l2q_ws; with Lk >= VT_MIN_KEYS and ATTN_VT, V is first
+    rewritten into the VT layout and prfl_attn_fwd_l2q_vt_ws runs)."""
     Lq, C = q.shape
     Lk = k.shape[0]
     assert C == num_heads * 128, "head_dim must be 128"
@@ -231,11 +238,24 @@ def attn_fwd(q, k, v, num_heads, k_len=None, out=None, scale=None, q_log2=False)
     head = (ptr(q), I64(_ld(q)), I64(0), ptr(k), I64(_ld(k)), I64(0), ptr(v), I64(_ld(v)), I64(0),
             ptr(out), I64(_ld(out)), I64(0), ptr(lse), I64(1), I64(Lq), I64(Lk), I64(num_heads),
             I64(k_len))
-    if q_log2:
+    if q_log2 and ATTN_VT and Lk >= VT_MIN_KEYS:
+        vt = attn_v_to_vt(v, num_heads)
+        call("prfl_attn_fwd_l2q_vt_ws", *head[:6], ptr(vt), *head[9:], ptr(ws), I64(nb), stream_ptr())
+    elif q_log2:
         call("prfl_attn_fwd_l2q_ws", *head, ptr(ws), I64(nb), stream_ptr())
     else:
         call("prfl_attn_fwd_ws", *head, F32(sc), ptr(ws), I64(nb), stream_ptr())
     return out, lse
+
+
+def attn_v_to_vt(v, num_heads):
+    """v [Lk, H*128] (row-strided view) -> its VT image (prfl_attn_v_to_vt), a flat bf16 tensor"""
+    Lk = v.shape[0]
+    nb = _lib.load().prfl_attn_vt_bytes(1, Lk, num_heads)
+    vt = torch.empty(nb // 2, dtype=BF16, device=v.device)
+    call("prfl_attn_v_to_vt", ptr(v), I64(_ld(v)), I64(0), ptr(vt), I64(1), I64(Lk), I64(num_heads),
+         stream_ptr())
+    return vt
 
 
 def attn_fwd_fp8(q, k, v, num_heads, k_len=None, out=None, scale=None, q_log2=False):

@@ -82,6 +82,20 @@ int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k, 
                          int64_t bk, const void* v, int64_t ldv, int64_t bv, void* o, int64_t ldo,
                          int64_t bo, float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
                          int64_t k_len, void* ws, int64_t ws_bytes, void* stream);
+/* V in the key-chunked transposed ("VT") layout of the long-KV self-attention forward: per
+ * (sample, head) [Lkp/8][128][8] bf16, Lkp = Lk rounded up to 96, the 8 keys of chunk 2j + h
+ * being 16j + 4h + {0,1,2,3,8,9,10,11}, zero past Lk.  Same reference interface as
+ * prfl_attn_fwd_ws (flash_attn_varlen_func, `wan/modules/attention.py:96-127`); prfl_attn_v_to_vt
+ * writes vt (prfl_attn_vt_bytes bytes, 16-B aligned) from v [B][Lk][H*128] (row stride ldv). */
+int64_t prfl_attn_vt_bytes(int64_t B, int64_t Lk, int64_t H);
+int prfl_attn_v_to_vt(const void* v, int64_t ldv, int64_t bv, void* vt, int64_t B, int64_t Lk,
+                      int64_t H, void* stream);
+/* prfl_attn_fwd_l2q_ws reading V from its VT image (Lk >= 4096 only, else hipErrorInvalidValue):
+ * every V^T fragment is one ds_read_b128; o / lse2 bit-identical to prfl_attn_fwd_l2q_ws. */
+int prfl_attn_fwd_l2q_vt_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                            int64_t bk, const void* vt, void* o, int64_t ldo, int64_t bo,
+                            float* lse2, int64_t B, int64_t Lq, int64_t Lk, int64_t H,
+                            int64_t k_len, void* ws, int64_t ws_bytes, void* stream);
 /* Config C5 (fp8): the same forward on the block-scaled e4m3 MFMA.  q, k, v stay bf16 in the
  * layout above and are quantised inside the call (Q per token and head, K per head, V per head
  * and channel, V stored transposed) into the REQUIRED caller-owned scratch `ws` (256-B aligned)

@@ -442,6 +442,67 @@ def test_attention_split_tail(ops):
     assert rel(dk[:klen, tail], rdk) < 2e-2 and rel(dv[:klen, tail], rdv) < 2e-2
 
 
+def _vt_image(v, H):
+    """torch restatement of prfl_attn_v_to_vt for one sample: v [Lk, H*128] -> [H][Lkp/8][128][8],
+    chunk 2j + h holding keys 16j + 4h + (0, 1, 2, 3, 8, 9, 10, 11), zero past Lk (Lkp = Lk
+    rounded up to 96)"""
+    Lk = v.shape[0]
+    lkp = (Lk + 95) // 96 * 96
+    vp = torch.zeros(lkp, H, 128, dtype=v.dtype, device=v.device)
+    vp[:Lk] = v.view(Lk, H, 128)
+    perm = torch.tensor([0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15], device=v.device)
+    x = vp.view(lkp // 16, 16, H, 128)[:, perm]                  # [j][h*8 + slot][H][d]
+    return x.view(lkp // 8, 8, H, 128).permute(2, 0, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("Lq,Lk,H,klen,B", [(4200, 4200, 2, 4133, 1), (4111, 5000, 1, 4500, 1),
+                                            (1000, 4100, 3, 4097, 2), (8100, 8100, 9, 8000, 1)])
+def test_attention_vt_bit_identical(ops, Lq, Lk, H, klen, B):
+    """The VT forward (prfl_attn_v_to_vt + prfl_attn_fwd_l2q_vt_ws: V^T fragments as one
+    ds_read_b128 from a key-chunked transposed image) against the row-major l2q forward: the
+    same operand values in the same k-slot order, so O and the LSE are bit-identical, including
+    ragged Lk (not a multiple of 96), k_len < Lk, two samples (sample strides) and the split-KV
+    tail (L = 8100, 9 heads); the transpose itself vs its torch restatement."""
+    from prfl_amd import _lib
+    C = H * 128
+    g = torch.Generator(device=DEV).manual_seed(Lq + Lk + B)
+    q2 = (torch.randn(B, Lq, C, generator=g, device=DEV) * 1.5 * SL2).to(torch.bfloat16)
+    k = (torch.randn(B, Lk, 3 * C, generator=g, device=DEV) * 1.5).to(torch.bfloat16)[:, :, :C]
+    v = torch.randn(B, Lk, 2 * C, generator=g, device=DEV).to(torch.bfloat16)[:, :, C:]  # strided
+    lkp = (Lk + 95) // 96 * 96
+    nb = _lib.load().prfl_attn_vt_bytes(B, Lk, H)
+    assert nb == B * H * lkp * 128 * 2
+    vt = torch.full((nb // 2,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    _lib.call("prfl_attn_v_to_vt", _lib.ptr(v), _lib.I64(2 * C), _lib.I64(Lk * 2 * C), _lib.ptr(vt),
+              _lib.I64(B), _lib.I64(Lk), _lib.I64(H), _lib.stream_ptr())
+    for b in range(B):
+        assert torch.equal(vt.view(B, H, lkp // 8, 128, 8)[b], _vt_image(v[b], H))
+    wsb = _lib.load().prfl_attn_fwd_ws_bytes(B, Lq, Lk, H, klen)
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=DEV)
+    outs = []
+    for use_vt in (False, True):
+        o = torch.empty(B, Lq, C, dtype=torch.bfloat16, device=DEV)
+        lse = torch.empty(B, H, Lq, device=DEV)
+        qk = (_lib.ptr(q2), _lib.I64(C), _lib.I64(Lq * C), _lib.ptr(k), _lib.I64(3 * C), _lib.I64(Lk * 3 * C))
+        tail = (_lib.ptr(o), _lib.I64(C), _lib.I64(Lq * C), _lib.ptr(lse), _lib.I64(B), _lib.I64(Lq),
+                _lib.I64(Lk), _lib.I64(H), _lib.I64(klen), _lib.ptr(ws), _lib.I64(wsb), _lib.stream_ptr())
+        if use_vt:
+            _lib.call("prfl_attn_fwd_l2q_vt_ws", *qk, _lib.ptr(vt), *tail)
+        else:
+            _lib.call("prfl_attn_fwd_l2q_ws", *qk, _lib.ptr(v), _lib.I64(2 * C), _lib.I64(Lk * 2 * C), *tail)
+        outs.append((o, lse))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # the ops-level path the fused block takes (ATTN_VT) against the row-major entry
+    o3, lse3 = ops.attn_fwd(q2[0], k[0], v[0], H, k_len=klen, q_log2=True)
+    assert torch.equal(o3, outs[0][0][0]) and torch.equal(lse3, outs[0][1][0])
+    # short KV has no VT instantiation: the entry refuses it
+    with pytest.raises(RuntimeError):
+        _lib.call("prfl_attn_fwd_l2q_vt_ws", _lib.ptr(q2), _lib.I64(C), _lib.I64(0), _lib.ptr(k),
+                  _lib.I64(3 * C), _lib.I64(0), _lib.ptr(vt), _lib.ptr(outs[0][0]), _lib.I64(C),
+                  _lib.I64(0), _lib.ptr(outs[0][1]), _lib.I64(1), _lib.I64(Lq), _lib.I64(512),
+                  _lib.I64(H), _lib.I64(512), _lib.ptr(None), _lib.I64(0), _lib.stream_ptr())
+
+
 def test_attention_rescale_spike(ops):
     """Force the online-softmax rescale: one key gets a huge score in a late tile (rule 26)."""
     L, C = 256, 128

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="time prfl_attn_fwd_fp8 (config C5) instead")
     ap.add_argument("--qs", default="", help="comma list of lib indices built with ATTN_QS=1: they "
                     "get q pre-scaled by softmax_scale * log2(e) (rounded to bf16 once)")
+    ap.add_argument("--vt", default="", help="comma list of lib indices to run through the VT entry "
+                    "(prfl_attn_v_to_vt + prfl_attn_fwd_l2q_vt_ws, the transpose inside the timing)")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     L, H, C = a.L, 40, 5120
@@ -52,7 +54,14 @@ def main():
             nb = lib.prfl_attn_fwd_ws_bytes(1, L, Lk, H, Lk)
             if "ws" not in b or b["ws"].numel() < nb:
                 b["ws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
-            if b.get("qs") and lib.has_l2q:
+            if b.get("vt"):
+                nv = lib.prfl_attn_vt_bytes(1, Lk, H)
+                if "vtb" not in b:
+                    b["vtb"] = torch.empty(nv, dtype=torch.uint8, device=dev)
+                assert lib.prfl_attn_v_to_vt(v.data_ptr(), 3 * C, 0, b["vtb"].data_ptr(), 1, Lk, H, st) == 0
+                assert lib.prfl_attn_fwd_l2q_vt_ws(*args[:6], b["vtb"].data_ptr(), *args[9:-1],
+                                                   b["ws"].data_ptr(), nb, st) == 0
+            elif b.get("qs") and lib.has_l2q:
                 assert lib.prfl_attn_fwd_l2q_ws(*args[:-1], b["ws"].data_ptr(), nb, st) == 0
             else:
                 assert lib.prfl_attn_fwd_ws(*args, b["ws"].data_ptr(), nb, st) == 0
@@ -80,6 +89,9 @@ def main():
 
     for i in qs_libs:
         outs[i]["qs"] = True
+    for i in {int(i) for i in a.vt.split(",") if i}:
+        assert i in qs_libs, "the VT entry takes q in log2 units"
+        outs[i]["vt"] = True
     work = [("fwd", fwd, 4 * L * Lk * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
     for w, fn, fl in work:
         ts = [[] for _ in libs]
