@@ -63,6 +63,8 @@ struct AttnBwdArgs {
   float* Pk;             // [dK/dV tail wg][256 keys][128] fp32 (dK^T partial)
   float* Pv;             // [dK/dV tail wg][256 keys][128] fp32
   float* Pq;             // [dQ tail wg][256 queries][128] fp32
+  const bf16* KT;        // KT dQ kernel: K in the VT layout of prfl_attn_v_to_vt (else unused)
+  int64_t bkt;           // its per (sample, head) stride, Lkp * 128
 };
 
 // (unit, share) of a 1-D grid whose workgroups >= nmain split the last units `split` ways
@@ -822,10 +824,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
 // LSE and D are per-lane scalars), dS^T = P^T (dP^T - D) packed to bf16, dQ^T += K^T dS^T.  The
 // K / V tiles arrive by LDS-DMA into a 2-stage ring (tile t+1 issued at the top of tile t,
 // retired by vmcnt(0) + the one barrier per tile).
-template <int NKT, bool QS>
+// KT: K^T fragments of dQ^T += K^T dS^T as one ds_read_b128 each from a third stage image, the
+// key-chunked transposed K (prfl_attn_v_to_vt of K; the forward's VT layout, whose k-slot order
+// is the dS^T fragment's), instead of two ds_read_b64_tr_b16 on the K row image (outputs
+// bit-identical; 72 KiB stages, two of them)
+template <int NKT, bool QS, bool KT = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
-  constexpr int TK = NKT * 32, SV = NKT * 8192, SB = 2 * SV;
-  constexpr int NST = ATTN_DQ_STAGES;                        // ring stages of [K (image B) | V]
+  constexpr int TK = NKT * 32, SV = NKT * 8192, SB = (KT ? 3 : 2) * SV;
+  constexpr int NST = KT ? 2 : ATTN_DQ_STAGES;               // ring stages of [K (image B) | V (| K^T)]
+  static_assert(!KT || (NKT == 3 && !ATTN_DQ_STAGGER), "KT: 2 stages of 96-key tiles");
   __shared__ __attribute__((aligned(16))) char smem[NST * SB];
   int unit, share;
   bool part;
@@ -842,6 +849,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const bf16* Kb = a.K + b * a.bk + h * HD;
   const bf16* Vb = a.V + b * a.bv + h * HD;
   const bf16* dOb = a.dO + b * a.bdo + h * HD;
+  const bf16* KTb = KT ? a.KT + ((int64_t)b * a.H + h) * a.bkt : nullptr;
   const int qr = min(q0 + w * 32 + l32, a.Lq - 1);
   bf16x8 qf[8], df[8];
 #pragma unroll
@@ -896,6 +904,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                 lds_addr(Ks + (w * NKT + i) * 1024));
       dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4), 0,
                 lds_addr(Vs + (w * NKT + i) * 1024));
+    }
+    if (KT) {          // K^T tile: one contiguous 24 KiB run, lane-linear pieces
+      const i32x4 skt = make_srd(KTb + (int64_t)t * TK * HD, (uint32_t)SV);
+#pragma unroll
+      for (int i = 0; i < NKT; ++i)
+        dma16_buf(skt, (uint32_t)((w * NKT + i) * 1024) + ln * 16, 0,
+                  lds_addr(Vs + SV + (w * NKT + i) * 1024));
     }
   };
   static_assert(!ATTN_DQ_STAGGER || NST == 3, "the dQ stagger needs the 3-stage ring");
@@ -972,7 +987,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
-          const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
+          const bf16x8 kf = KT ? *(const bf16x8*)(Vs + SV + (kt * 4 + 2 * s2 + hh) * 2048 + (dt * 32 + l32) * 16)
+                               : cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
           dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
         }
       }
@@ -1876,9 +1892,10 @@ int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                   void* dq, int64_t lddq, int64_t bdq, void* dk, int64_t lddk, int64_t bdk,
                   void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq, int64_t Lk,
                   int64_t H, int64_t k_len, float scale, bool l2q, void* ws, int64_t ws_bytes,
-                  void* stream) {
+                  void* stream, const void* kt = nullptr) {
   if (B <= 0 || Lq <= 0 || H <= 0) return 0;
   if (Lk <= 0 || k_len <= 0 || k_len > Lk) return (int)hipErrorInvalidValue;
+  if (kt && (!l2q || Lk < 4096 || !aligned16(kt))) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
       !aligned16(dq) || !aligned16(dk) || !aligned16(dv) || !aligned16(ws) ||
       (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8)
@@ -1906,7 +1923,8 @@ int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                 (const bf16*)dout, lddo, bdo, lse2, delta, (bf16*)dq, lddq, bdq, (bf16*)dk, lddk,
                 bdk, (bf16*)dv, lddv, bdv, (int)Lq, (int)Lk, (int)H, (int)k_len,
                 l2q ? 1.f : scale * 1.4426950408889634f, l2q ? 0.6931471805599453f : scale,
-                (int)B, nmain_k, split_k, nmain_q, split_q, Pk, Pv, Pq};
+                (int)B, nmain_k, split_k, nmain_q, split_q, Pk, Pv, Pq, (const bf16*)kt,
+                vt_keys(Lk) * HD};
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
   if (l2q)
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, dim3((unsigned)(nmain_k + rk * split_k)), dim3(512), 0, s, a);
@@ -1917,7 +1935,9 @@ int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
   prfl_prof::end(KID_ATTN_BWD_DKDV, s);
   PRFL_LAUNCH_CHECK();
   prfl_prof::begin(KID_ATTN_BWD_DQ, s);
-  if (l2q)
+  if (kt)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
+  else if (l2q)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, false>), dim3((unsigned)(nmain_q + rq * split_q)), dim3(512), 0, s, a);
@@ -1956,6 +1976,23 @@ extern "C" int prfl_attn_bwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, cons
   return attn_bwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, dout, lddo, bdo, lse2,
                        delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
                        1.f, true, ws, ws_bytes, stream);
+}
+
+// prfl_attn_bwd_l2q_ws with K also in the VT layout (kt = prfl_attn_v_to_vt of k; Lk >= 4096):
+// the dQ kernel reads its K^T fragments as one ds_read_b128 each; outputs bit-identical
+extern "C" int prfl_attn_bwd_l2q_kt_ws(const void* q, int64_t ldq, int64_t bq, const void* k,
+                                       int64_t ldk, int64_t bk, const void* kt, const void* v,
+                                       int64_t ldv, int64_t bv, const void* o, int64_t ldo,
+                                       int64_t bo, const void* dout, int64_t lddo, int64_t bdo,
+                                       const float* lse2, float* delta, void* dq, int64_t lddq,
+                                       int64_t bdq, void* dk, int64_t lddk, int64_t bdk, void* dv,
+                                       int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
+                                       int64_t Lk, int64_t H, int64_t k_len, void* ws,
+                                       int64_t ws_bytes, void* stream) {
+  if (!kt) return (int)hipErrorInvalidValue;
+  return attn_bwd_impl(q, ldq, bq, k, ldk, bk, v, ldv, bv, o, ldo, bo, dout, lddo, bdo, lse2,
+                       delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
+                       1.f, true, ws, ws_bytes, stream, kt);
 }
 
 extern "C" int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H,

@@ -44,6 +44,9 @@ SIGNATURES = {
     "prfl_attn_bwd_l2q_ws": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P,
                              P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, P, I64,
                              P],
+    "prfl_attn_bwd_l2q_kt_ws": [P, I64, I64, P, I64, I64, P, P, I64, I64, P, I64, I64, P, I64, I64,
+                                P, P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64,
+                                I64, P, I64, P],
     "prfl_attn_bwd": [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, P, P, P, I64,
                       I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],

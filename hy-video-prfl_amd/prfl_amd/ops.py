@@ -216,6 +216,9 @@ def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_s
 # the long-KV q_log2 forward reads V from its key-chunked transposed image (prfl_attn_v_to_vt +
 # prfl_attn_fwd_l2q_vt_ws: one ds_read_b128 per V^T fragment; outputs bit-identical)
 ATTN_VT = True
+# ... and the long-KV q_log2 backward's dQ kernel its K^T fragments from K's VT image
+# (prfl_attn_bwd_l2q_kt_ws; outputs bit-identical)
+ATTN_KT = True
 VT_MIN_KEYS = 4096
 
 
@@ -300,7 +303,10 @@ def attn_bwd(q, k, v, o, do, lse, num_heads, k_len=None, dq=None, dk=None, dv=No
             ptr(o), I64(_ld(o)), I64(0), ptr(do), I64(_ld(do)), I64(0), ptr(lse), ptr(delta),
             ptr(dq), I64(_ld(dq)), I64(0), ptr(dk), I64(_ld(dk)), I64(0), ptr(dv), I64(_ld(dv)),
             I64(0), I64(1), I64(Lq), I64(Lk), I64(num_heads), I64(k_len))
-    if q_log2:
+    if q_log2 and ATTN_KT and Lk >= VT_MIN_KEYS:
+        kt = attn_v_to_vt(k, num_heads)            # K in the VT layout for the dQ kernel
+        call("prfl_attn_bwd_l2q_kt_ws", *head[:6], ptr(kt), *head[6:], ptr(ws), I64(nb), stream_ptr())
+    elif q_log2:
         call("prfl_attn_bwd_l2q_ws", *head, ptr(ws), I64(nb), stream_ptr())
     else:
         call("prfl_attn_bwd_ws", *head, F32(sc), ptr(ws), I64(nb), stream_ptr())

@@ -133,6 +133,17 @@ int prfl_attn_bwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int6
                      int64_t bdk, void* dv, int64_t lddv, int64_t bdv, int64_t B, int64_t Lq,
                      int64_t Lk, int64_t H, int64_t k_len, float scale, void* ws,
                      int64_t ws_bytes, void* stream);
+/* prfl_attn_bwd_l2q_ws with K also given in the VT layout (kt = prfl_attn_v_to_vt of k, the same
+ * [B][Lk][H*128] tensor; Lk >= 4096 only): the dQ kernel reads its K^T fragments as one
+ * ds_read_b128 each; outputs bit-identical to prfl_attn_bwd_l2q_ws.  Same reference interface
+ * (flash_attn's varlen backward). */
+int prfl_attn_bwd_l2q_kt_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
+                            int64_t bk, const void* kt, const void* v, int64_t ldv, int64_t bv,
+                            const void* o, int64_t ldo, int64_t bo, const void* dout, int64_t lddo,
+                            int64_t bdo, const float* lse2, float* delta, void* dq, int64_t lddq,
+                            int64_t bdq, void* dk, int64_t lddk, int64_t bdk, void* dv,
+                            int64_t lddv, int64_t bdv, int64_t B, int64_t Lq, int64_t Lk,
+                            int64_t H, int64_t k_len, void* ws, int64_t ws_bytes, void* stream);
 /* Scratch bytes prfl_attn_bwd_ws needs on the current device (0 = no split for this shape). */
 int64_t prfl_attn_bwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
 /* prfl_attn_bwd_ws for a q in log2 units (prfl_attn_fwd_l2q_ws): dq is the gradient w.r.t. that

@@ -503,6 +503,32 @@ def test_attention_vt_bit_identical(ops, Lq, Lk, H, klen, B):
                   _lib.I64(H), _lib.I64(512), _lib.ptr(None), _lib.I64(0), _lib.stream_ptr())
 
 
+@pytest.mark.parametrize("Lq,Lk,H,klen", [(4200, 4200, 2, 4133), (4111, 5000, 1, 4500),
+                                          (8100, 8100, 9, 8000)])
+def test_attention_kt_backward_bit_identical(ops, Lq, Lk, H, klen):
+    """The KT backward (prfl_attn_bwd_l2q_kt_ws: the dQ kernel's K^T fragments from K's VT image,
+    one ds_read_b128 each) against the row-major l2q backward: dq, dk, dv bit-identical, incl.
+    ragged Lk, k_len < Lk and the split tails (L = 8100, 9 heads)."""
+    from prfl_amd import ops as O_
+    g = torch.Generator(device=DEV).manual_seed(Lq * 5 + Lk)
+    C = H * 128
+    q2 = (torch.randn(Lq, C, generator=g, device=DEV) * 1.5 * SL2).to(torch.bfloat16)
+    k = (torch.randn(Lk, C, generator=g, device=DEV) * 1.5).to(torch.bfloat16)
+    v = torch.randn(Lk, C, generator=g, device=DEV).to(torch.bfloat16)
+    do = torch.randn(Lq, C, generator=g, device=DEV).to(torch.bfloat16)
+    o, lse = ops.attn_fwd(q2, k, v, H, k_len=klen, q_log2=True)
+    got = []
+    saved = O_.ATTN_KT
+    try:
+        for kt in (False, True):
+            O_.ATTN_KT = kt
+            got.append(ops.attn_bwd(q2, k, v, o, do, lse, H, k_len=klen, q_log2=True))
+    finally:
+        O_.ATTN_KT = saved
+    for a, b in zip(*got):
+        assert torch.equal(a, b)
+
+
 def test_attention_rescale_spike(ops):
     """Force the online-softmax rescale: one key gets a huge score in a late tile (rule 26)."""
     L, C = 256, 128

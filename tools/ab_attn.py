@@ -41,6 +41,10 @@ def load(path):
         lib.prfl_attn_fwd_l2q_vt_ws.restype = ctypes.c_int
         lib.prfl_attn_v_to_vt.argtypes, lib.prfl_attn_v_to_vt.restype = [P, I64, I64, P, I64, I64, I64, P], ctypes.c_int
         lib.prfl_attn_vt_bytes.argtypes, lib.prfl_attn_vt_bytes.restype = [I64] * 3, I64
+    lib.has_kt = hasattr(lib, "prfl_attn_bwd_l2q_kt_ws")
+    if lib.has_kt:
+        lib.prfl_attn_bwd_l2q_kt_ws.argtypes = BWD[:6] + [P] + BWD[6:-2] + [P, I64, P]
+        lib.prfl_attn_bwd_l2q_kt_ws.restype = ctypes.c_int
     lib.has_bws = hasattr(lib, "prfl_attn_bwd_ws")
     if lib.has_bws:
         lib.prfl_attn_bwd_ws.argtypes, lib.prfl_attn_bwd_ws.restype = BWD[:-1] + [P, I64, P], ctypes.c_int

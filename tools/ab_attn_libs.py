@@ -80,7 +80,14 @@ def main():
             nb = lib.prfl_attn_bwd_ws_bytes(1, L, L, H, L)
             if "bws" not in b or b["bws"].numel() < nb:
                 b["bws"] = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
-            if b.get("qs") and lib.has_l2q:
+            if b.get("vt") and lib.has_kt:     # VT libs also take the KT backward
+                nv = lib.prfl_attn_vt_bytes(1, L, H)
+                if "ktb" not in b:
+                    b["ktb"] = torch.empty(nv, dtype=torch.uint8, device=dev)
+                assert lib.prfl_attn_v_to_vt(k.data_ptr(), 3 * C, 0, b["ktb"].data_ptr(), 1, L, H, st) == 0
+                assert lib.prfl_attn_bwd_l2q_kt_ws(*args[:6], b["ktb"].data_ptr(), *args[6:-1],
+                                                   b["bws"].data_ptr(), nb, st) == 0
+            elif b.get("qs") and lib.has_l2q:
                 assert lib.prfl_attn_bwd_l2q_ws(*args[:-1], b["bws"].data_ptr(), nb, st) == 0
             else:
                 assert lib.prfl_attn_bwd_ws(*args, b["bws"].data_ptr(), nb, st) == 0
