@@ -673,6 +673,13 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 #ifndef GEMM4_PREWAIT
 #define GEMM4_PREWAIT 1
 #endif
+#ifndef GEMM4_IL
+#define GEMM4_IL 0
+#endif
+// AGPR-accumulator MFMA as inline asm ("+a" keeps hipcc from moving the accumulators to VGPRs)
+__device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
@@ -746,6 +753,24 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if (GEMM4_IL) {
+        // hipBLASLt's placement (its TN loop, disassembled): every non-MFMA instruction sits
+        // BETWEEN two MFMAs, so the matrix pipe has the next product queued behind it
+        mfma16(acc[i][0], cb[0], ca[i]);
+        piece(i, jd, sd);
+        mfma16(acc[i][1], cb[1], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16(acc[i][2], cb[2], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jj = 3; jj < 8; ++jj) mfma16(acc[i][jj], cb[jj], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       piece(i, jd, sd);
       na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
       nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);

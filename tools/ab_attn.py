@@ -37,7 +37,7 @@ def load(path):
         lib.prfl_attn_bwd_l2q_ws.restype = ctypes.c_int
     lib.has_vt = hasattr(lib, "prfl_attn_fwd_l2q_vt_ws")
     if lib.has_vt:    # V in the key-chunked transposed layout (round 4)
-        lib.prfl_attn_fwd_l2q_vt_ws.argtypes = FWD[:6] + FWD[9:-2] + [P, I64, P]
+        lib.prfl_attn_fwd_l2q_vt_ws.argtypes = FWD[:6] + [P] + FWD[9:-2] + [P, I64, P]
         lib.prfl_attn_fwd_l2q_vt_ws.restype = ctypes.c_int
         lib.prfl_attn_v_to_vt.argtypes, lib.prfl_attn_v_to_vt.restype = [P, I64, I64, P, I64, I64, I64, P], ctypes.c_int
         lib.prfl_attn_vt_bytes.argtypes, lib.prfl_attn_vt_bytes.restype = [I64] * 3, I64
