@@ -390,12 +390,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
             o[dt] = mfma32(vf, pf[kt][s2], o[dt]);
           }
       }
-      if (SCHED) {   // V^T transposed reads SCHED+1 MFMAs ahead, two per MFMA gap
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * SCHED + 2, 1);
+      if (SCHED) {   // V^T reads SCHED+1 MFMAs ahead: two transposed reads (VT: one b128) per gap
+        constexpr int RPM = VT ? 1 : 2;
+        __builtin_amdgcn_sched_group_barrier(0x100, RPM * (SCHED + 1), 1);
 #pragma unroll
         for (int i = 0; i < NKT * 8 - 1 - SCHED; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, RPM, 1);
         }
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }

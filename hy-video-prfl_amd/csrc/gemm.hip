@@ -673,8 +673,12 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 #ifndef GEMM4_PREWAIT
 #define GEMM4_PREWAIT 1
 #endif
+// 1: every non-MFMA instruction of the four-wave loop between two MFMAs, as hipBLASLt's TN
+// loop places them (one LDS-DMA piece after MFMA 0, the A / B fragment reads after MFMAs 1 / 2 of
+// each 8-MFMA chunk) instead of a [piece, reads, 8 MFMAs] burst: bit-identical, forward +0.2-1.7 %,
+// dX +1.1-6.7 % on the 720p shapes (profiles/r04_ab_gemm_il.txt)
 #ifndef GEMM4_IL
-#define GEMM4_IL 0
+#define GEMM4_IL 1
 #endif
 // AGPR-accumulator MFMA as inline asm ("+a" keeps hipcc from moving the accumulators to VGPRs)
 __device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
@@ -753,6 +757,24 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     // over the slice (one wave per SIMD: nothing else fills the matrix pipe)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if (GEMM4_IL == 2) {    // the slice's 8 pieces in its first half, two per chunk
+        mfma16(acc[i][0], cb[0], ca[i]);
+        if (i < 4) piece(2 * i, jd, sd);
+        mfma16(acc[i][1], cb[1], ca[i]);
+        if (i < 4) piece(2 * i + 1, jd, sd);
+        mfma16(acc[i][2], cb[2], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        na[i] = read_frag4<A_KC>(st, wm * 128 + i * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16(acc[i][3], cb[3], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        nb[i] = read_frag4<B_KC>(st + HALF4, wn * 128 + i * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jj = 4; jj < 8; ++jj) mfma16(acc[i][jj], cb[jj], ca[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       if (GEMM4_IL) {
         // hipBLASLt's placement (its TN loop, disassembled): every non-MFMA instruction sits
         // BETWEEN two MFMAs, so the matrix pipe has the next product queued behind it

@@ -215,10 +215,11 @@ def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_s
 
 # the long-KV q_log2 forward reads V from its key-chunked transposed image (prfl_attn_v_to_vt +
 # prfl_attn_fwd_l2q_vt_ws: one ds_read_b128 per V^T fragment; outputs bit-identical)
-ATTN_VT = True
-# ... and the long-KV q_log2 backward's dQ kernel its K^T fragments from K's VT image
-# (prfl_attn_bwd_l2q_kt_ws; outputs bit-identical)
-ATTN_KT = True
+ATTN_VT = True     # 720p forward 84.11 -> 83.08 ms incl. the 0.29 ms transpose (profiles/r04_ab_attn_vt.txt)
+# ... and (off) the long-KV q_log2 backward's dQ kernel its K^T fragments from K's VT image
+# (prfl_attn_bwd_l2q_kt_ws; bit-identical, measured 0.3-0.5 % slower with the K transpose
+# included: profiles/r04_ab_bwd_variants.txt)
+ATTN_KT = False
 VT_MIN_KEYS = 4096
 
 

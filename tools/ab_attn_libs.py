@@ -99,6 +99,20 @@ def main():
     for i in {int(i) for i in a.vt.split(",") if i}:
         assert i in qs_libs, "the VT entry takes q in log2 units"
         outs[i]["vt"] = True
+    for i in sorted(j for j in range(len(libs)) if outs[j].get("vt")):   # the transpose alone
+        lib = libs[i]
+        vtb = torch.empty(lib.prfl_attn_vt_bytes(1, Lk, H), dtype=torch.uint8, device=dev)
+        ts = []
+        for r in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert lib.prfl_attn_v_to_vt(v.data_ptr(), 3 * C, 0, vtb.data_ptr(), 1, Lk, H, st) == 0
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                ts.append(e0.elapsed_time(e1))
+        m = statistics.median(ts)
+        print(f"v_to_vt lib{i}: {m:.3f} ms ({2 * Lk * C * 2 / m / 1e6:.0f} GB/s)", flush=True)
     work = [("fwd", fwd, 4 * L * Lk * C)] + ([("bwd", bwd, 10 * L * L * C)] if a.bwd else [])
     for w, fn, fl in work:
         ts = [[] for _ in libs]
