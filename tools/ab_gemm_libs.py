@@ -46,7 +46,17 @@ def main():
                      dw=torch.empty(N, K, device=dev)) for _ in libs]
         fl = 2 * L * N * K
 
+        wt = w.t().contiguous()     # [K, N]: the weight as an MN-major B operand
+
         def call(lib, o, pas):
+            if pas.endswith("_t"):    # forward passes on the transposed weight (MN-major B)
+                epi = {"fwd_t": 0, "gelu_t": 1, "resid_t": 2}[pas]
+                rc = lib.prfl_gemm_bf16_tiled(x.data_ptr(), K, 1, wt.data_ptr(), N, 0, o.data_ptr(), N, L, N, K,
+                                              epi, None, gate.data_ptr() if epi == 2 else None,
+                                              res.data_ptr() if epi == 2 else None, N, 0,
+                                              aux.data_ptr() if epi else None, N, 0, tile_of[id(lib)], st)
+                assert rc == 0, rc
+                return
             if pas == "fwd":   # y[L,N] = x[L,K] w[N,K]^T
                 args = (x.data_ptr(), K, 1, w.data_ptr(), K, 1, o.data_ptr(), N, L, N, K, 0)
             elif pas == "dx":  # dx[L,K] = dy[L,N] w[N,K]
@@ -87,6 +97,9 @@ def main():
             o["gelu"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
             o["resid"] = torch.empty(L, N, device=dev)
             o["dwacc"] = torch.zeros(N, K, device=dev)
+            o["fwd_t"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+            o["gelu_t"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+            o["resid_t"] = torch.empty(L, N, device=dev)
         for pas in a.passes.split(","):
             ts = [[] for _ in libs]
             for r in range(a.reps + 1):
@@ -107,6 +120,9 @@ def main():
             print(f"{name:5s} {pas:3s}: " + " | ".join(f"lib{i} {m:6.2f} ms {fl / m / 1e9:5.0f} TF/s"
                                                        for i, m in enumerate(meds))
                   + f" | identical {same}", flush=True)
+        for pa, pb in (("fwd", "fwd_t"), ("gelu", "gelu_t"), ("resid", "resid_t")):
+            if pa in a.passes.split(",") and pb in a.passes.split(","):
+                print(f"{name:5s} {pa} vs {pb}: identical {torch.equal(outs[0][pa], outs[0][pb])}", flush=True)
         del x, w, dy, outs
 
 
