@@ -1176,6 +1176,8 @@ extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, co
   GEMM_CASE(1, 1, EPI_F32)
   GEMM_CASE(1, 1, EPI_DGELU)
   GEMM_CASE(1, 0, EPI_BF16)
+  GEMM_CASE(1, 0, EPI_GELU)
+  GEMM_CASE(1, 0, EPI_RESID)
   GEMM_CASE(1, 0, EPI_DGELU)
   GEMM_CASE(1, 0, EPI_F32)
   GEMM_CASE(0, 0, EPI_F32)

@@ -45,6 +45,17 @@ def linear(x, w, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None, au
     return gemm(x, w, out, M, N, K, True, True, epilogue, bias, gate, res, aux, tile=tile)
 
 
+def linear_t(x, wt, bias=None, epilogue=EPI_BF16, out=None, gate=None, res=None, aux=None):
+    """linear() on the transposed weight wt [K, N] (cast_bf16_t of the nn.Linear weight): the
+    weight is then an MN-major GEMM operand; results bit-identical to linear(x, wt.t())."""
+    M, K = x.shape
+    N = wt.shape[1]
+    if out is None:
+        dt = torch.float32 if epilogue in (EPI_RESID, EPI_F32) else BF16
+        out = torch.empty(M, N, dtype=dt, device=x.device)
+    return gemm(x, wt, out, M, N, K, True, False, epilogue, bias, gate, res, aux)
+
+
 def linear_dx(dy, w, out=None, epilogue=EPI_BF16, aux=None):
     """dX[M,K] = dY[M,N] @ W[N,K] (bf16 out; DGELU epilogue multiplies by gelu'(aux))."""
     M, N = dy.shape
@@ -110,6 +121,20 @@ def cast_bf16(src, dst=None):
         dst = torch.empty(src.shape, dtype=BF16, device=src.device)
     assert dst.is_contiguous() and dst.numel() == src.numel()
     call("prfl_cast_f32_bf16", ptr(src), ptr(dst), I64(src.numel()), stream_ptr())
+    return dst
+
+
+def cast_bf16_t(w, dst=None):
+    """fp32 nn.Linear weight w [N, K] -> bf16 w^T [K, N] (prfl_cast_f32_bf16_t); dst may be a
+    column block of a wider row-major buffer (its row stride is dst.stride(0))."""
+    _lib.require_gpu(w)
+    w = w.contiguous()
+    N, K = w.shape
+    if dst is None:
+        dst = torch.empty(K, N, dtype=BF16, device=w.device)
+    assert dst.shape == (K, N) and dst.stride(1) == 1
+    call("prfl_cast_f32_bf16_t", ptr(w), I64(N), I64(K), I64(K), ptr(dst), I64(dst.stride(0)),
+         stream_ptr())
     return dst
 
 

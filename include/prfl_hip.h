@@ -221,6 +221,12 @@ int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const void* x, int6
 /* ---- element-wise / reductions ------------------------------------------------------------ */
 /* autocast weight cast fp32 -> bf16 (the .to(bf16) of every Linear weight under autocast). */
 int prfl_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
+/* The same cast into the transposed layout: out[k * ldo + n] = bf16(w[n * ldw + k]) for an fp32
+ * nn.Linear weight w [N][K] — the forward projection's weight as an MN-major prfl_gemm_bf16
+ * operand (b_kmajor = 0, ldb = ldo), bit-identical results to the K-major form.  ldw % 4,
+ * ldo % 8 == 0, 16-B aligned pointers. */
+int prfl_cast_f32_bf16_t(const float* w, int64_t N, int64_t K, int64_t ldw, void* out, int64_t ldo,
+                         void* stream);
 /* backward of the gated residual x + y*gate (model.py:348, :355): dy = bf16(dx*gate);
  * partial column sums of dx*y (-> d gate) and of dy (-> d bias of the producing Linear). */
 int prfl_gate_bwd(const float* dx, int64_t lddx, const void* y, int64_t ldy, const float* gate,

@@ -165,6 +165,33 @@ def test_gemm_backward_layouts(ops, M, N, K):
     assert rel(dg, p.grad) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 512), (73920, 5120, 5120), (2000, 768, 1280),
+                                   (300, 512, 384)])
+def test_linear_transposed_weight_bit_identical(ops, M, N, K):
+    """The forward projections on the transposed weight (ops.cast_bf16_t + ops.linear_t: W^T as
+    an MN-major operand, block.BF16Weights) against linear() on the K-major weight: outputs and
+    aux bit-identical for the bf16 / GELU / gated-residual (fp32 and bf16 residual) epilogues,
+    incl. the 128-tile fallback (M, K off the 256 grid); the transposing cast vs torch's."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    w32 = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    bias = (torch.randn(N, generator=g, device=DEV) * 0.1).to(torch.bfloat16)
+    wt = ops.cast_bf16_t(w32)
+    assert torch.equal(wt, w32.t().to(torch.bfloat16))
+    wk = ops.cast_bf16(w32)
+    assert torch.equal(ops.linear_t(x, wt, bias), ops.linear(x, wk, bias))
+    a0, a1 = (torch.empty(M, N, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    assert torch.equal(ops.linear_t(x, wt, bias, ops.EPI_GELU, aux=a0),
+                       ops.linear(x, wk, bias, ops.EPI_GELU, aux=a1))
+    assert torch.equal(a0, a1)
+    gate = torch.randn(N, generator=g, device=DEV)
+    for res in (torch.randn(M, N, generator=g, device=DEV),
+                torch.randn(M, N, generator=g, device=DEV).to(torch.bfloat16)):
+        y0 = ops.linear_t(x, wt, bias, ops.EPI_RESID, gate=gate, res=res, aux=a0)
+        y1 = ops.linear(x, wk, bias, ops.EPI_RESID, gate=gate, res=res, aux=a1)
+        assert torch.equal(y0, y1) and torch.equal(a0, a1)
+
+
 def test_gemm_identity_asymmetric(ops):
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     n = 128
