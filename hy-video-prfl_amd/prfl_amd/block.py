@@ -100,9 +100,11 @@ class BF16Weights:
         # bf16 path: the six forward projections take their weight TRANSPOSED (self.t[name] =
         # W^T [K, N], cast straight from the fp32 master by ops.cast_bf16_t): an MN-major GEMM
         # operand, bit-identical results, 2-4 % faster forward GEMMs (profiles/r04_ab_gemm_wt.txt);
-        # the K-major copies (self.w*) are cast only where a backward's dX GEMM reads them
+        # the K-major copies (self.w*) are cast only where a backward's dX GEMM reads them, and
+        # there (need_bf16: the backward's recompute, 88 of the 928 block forwards of a 720p
+        # iteration) the forward reuses them: no second copy of the block's weights at the peak
         self.t = {}
-        if not fp8:
+        if not fp8 and not need_bf16:
             wt = lambda n: ops.cast_bf16_t(g(n)) if g(n).shape[0] % 256 == 0 else None  # noqa: E731
             if C % 256 == 0:
                 self.t["qkv"] = torch.empty(C, 3 * C, dtype=BF16, device=dev)
