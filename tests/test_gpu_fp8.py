@@ -222,6 +222,64 @@ def test_block_fp8_vs_fp32_truth():
     assert e16_vs_oracle["update"] < 1e-2 and e16_vs_oracle["dx"] < 3e-2, e16_vs_oracle
 
 
+def test_fp8_error_across_a_block_chain():
+    """Does config C5's per-block error compound over depth?  Four real-width I2V blocks (C =
+    5120, 40 heads, independent weights) chained at L = 4 200, no grad: after every block the
+    cumulative residual update x_k - x_0 of the fp8 path (e4m3 projections AND the int8 / e4m3
+    self-attention forward, block.Meta fp8 = 2) and of the bf16 path, both against the oracle's
+    fp32 truth chain (every cast point removed).  Held to the single-block rule at every depth
+    (fp8 <= 16 x bf16 and <= 1e-1), and to NO compounding: the fp8 chain's error after four
+    blocks stays within 1.5 x its error after one (the e4m3 roundings of different blocks are
+    independent, so the relative error of the summed update does not grow with depth; a
+    compounding bias would).  VERDICT r03 weak #8: 'nothing measures what 5 % per block does
+    across 40 blocks'."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from shapes import block_shapes, seeded_params
+    from oracle import wan_oracle as O
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    torch.set_num_threads(16)
+    C, Fd, nh, i2v, depth = 5120, 13824, 40, True, 4
+    grid = (3, 35, 40)
+    L = grid[0] * grid[1] * grid[2]
+    names = B.param_names(i2v)
+    g = torch.Generator().manual_seed(21)
+    x0 = torch.randn(1, L, C, generator=g)
+    ctx = torch.randn(1, 512 + 257, C, generator=g).to(torch.bfloat16)
+    rope = ops.rope_table(O.rope_freqs(128), DEV)
+    xs = {"truth": x0.clone(), 0: x0.to(DEV), 2: x0.to(DEV)}
+    errs = {0: [], 2: []}
+    saved = O.bf
+    for k in range(depth):
+        P = seeded_params(block_shapes("b.", C, Fd, i2v), prefix=f"fp8chain{k}.")
+        e0 = torch.randn(1, 6, C, generator=g) * 0.1
+        O.bf = lambda t: t
+        try:
+            with torch.no_grad():
+                xs["truth"] = O.block_forward(P, "b.", xs["truth"], e0, torch.tensor([grid]),
+                                              O.rope_freqs(128), ctx.float(), nh, seq_len=L, i2v=i2v)
+        finally:
+            O.bf = saved
+        Pd = {n: P["b." + n].to(DEV) for n in names}
+        e = (e0 + P["b.modulation"]).to(DEV)
+        for fp8 in (0, 2):
+            meta = B.Meta(nh, [grid], [L], rope, i2v, fp8=fp8)
+            with torch.no_grad():
+                xs[fp8] = B.block_apply(Pd, xs[fp8], e, ctx.to(DEV), meta)
+        del Pd, P
+        upd_t = xs["truth"] - x0
+        for fp8 in (0, 2):
+            errs[fp8].append(rel((xs[fp8] - x0.to(DEV)).cpu(), upd_t))
+    print("cumulative-update error vs the fp32 truth per depth: bf16", [round(v, 4) for v in errs[0]],
+          "fp8", [round(v, 4) for v in errs[2]])
+    for k in range(depth):
+        assert errs[2][k] <= 16 * errs[0][k] and errs[2][k] <= 1e-1, (k, errs[2][k], errs[0][k])
+        assert errs[0][k] < 1e-2, (k, errs[0][k])
+    assert errs[2][-1] <= 1.5 * errs[2][0], errs[2]
+
+
 # ------------------------------------------------- low-precision self-attention forward (C5) --
 def _quant_ref(q, k, v, H, klen=None):
     """The kernel's quantisation restated in torch (prfl_attn_fwd_fp8's prologue): Q int8 per
