@@ -105,8 +105,9 @@ class BF16Weights:
         # iteration) the forward reuses them: no second copy of the block's weights at the peak
         self.t = {}
         if not fp8 and not need_bf16:
-            wt = lambda n: ops.cast_bf16_t(g(n)) if g(n).shape[0] % 256 == 0 else None  # noqa: E731
-            if C % 256 == 0:
+            f32 = lambda n: g(n).dtype == torch.float32  # noqa: E731  (bf16-stored: K-major path)
+            wt = lambda n: ops.cast_bf16_t(g(n)) if f32(n) and g(n).shape[0] % 256 == 0 else None  # noqa: E731
+            if C % 256 == 0 and all(f32(f"self_attn.{n}.weight") for n in "qkv"):
                 self.t["qkv"] = torch.empty(C, 3 * C, dtype=BF16, device=dev)
                 for i, n in enumerate("qkv"):
                     ops.cast_bf16_t(g(f"self_attn.{n}.weight"), self.t["qkv"][:, i * C:(i + 1) * C])

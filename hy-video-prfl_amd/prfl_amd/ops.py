@@ -114,9 +114,16 @@ def linear_fp8(xq, xs, wq, ws, bias=None, epilogue=EPI_BF16, out=None, gate=None
 
 
 def cast_bf16(src, dst=None):
-    """fp32 -> bf16 (round to nearest even); dst may be a contiguous slice of a larger buffer."""
+    """fp32 -> bf16 (round to nearest even); dst may be a contiguous slice of a larger buffer.
+    A weight already stored in bf16 (a frozen trunk, train.store_frozen_bf16) is returned as
+    it is, or copied into dst: its bits are what the cast of its fp32 master would give."""
     _lib.require_gpu(src)
     src = src.contiguous()
+    if src.dtype == BF16:
+        if dst is None:
+            return src
+        assert dst.is_contiguous() and dst.numel() == src.numel()
+        return dst.view(src.shape).copy_(src)
     if dst is None:
         dst = torch.empty(src.shape, dtype=BF16, device=src.device)
     assert dst.is_contiguous() and dst.numel() == src.numel()

@@ -43,11 +43,13 @@ def default_stash(model, world):
 
 def analytic(world, stash_gb, model="t2v"):
     act = L * C * 4 / GB                                   # one fp32 residual [L, C]
-    p_lrm = 8 * BLOCK[model] + (P_GEN[model] - NL * BLOCK[model])   # 8 blocks + embeddings
+    p_emb = P_GEN[model] - NL * BLOCK[model]                        # embeddings + head
     rows = {
         "fp32 generator params": P_GEN[model] * 4 / GB,
         "fp32 generator grads (persistent, accumulated in place)": P_GEN[model] * 4 / GB,
-        "fp32 reward-model trunk + head (frozen, no grads)": (p_lrm + P_HEAD) * 4 / GB,
+        # round 4: the frozen trunk's block Linear weights live in bf16 (train.store_frozen_bf16)
+        "reward-model trunk (8 blocks, bf16 weights) + fp32 embeddings + head (frozen)":
+            (8 * BLOCK[model] * 2 + (p_emb + P_HEAD) * 4) / GB,
         "40 generator + 8 LRM block-input checkpoints (fp32)": (NL + 8) * act,
         "attention-output stash (budget)": stash_gb,
         "one block's recompute + backward working set": 20.0,
