@@ -201,10 +201,11 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_FWD_SCHED
 #define ATTN_FWD_SCHED 3
 #endif
-// VT forward: the LDS reads placed in groups of RGRP per RGRP MFMAs (1 = one per gap): a group
-// lets the compiler's waitcnt pass cover RGRP MFMAs with one s_waitcnt instead of one each
+// VT forward: the LDS reads placed in groups of RGRP per RGRP MFMAs (1 = one per gap).  2: 720p
+// forward 85.09 -> 84.83 ms, bit-identical; on the VT kernel G0_DMA_Y 0 is 6.4 % and lazy tau
+// 10 0.5 % slower, SCHED 4 ties (profiles/r04_ab_attn_vt_knobs.txt)
 #ifndef ATTN_FWD_RGRP
-#define ATTN_FWD_RGRP 1
+#define ATTN_FWD_RGRP 2
 #endif
 // 1: waves 0-3 issue their half of tile t+1 in Y_t (their softmax phase, VALU only) instead of
 // X_t, beside MFMAs and LDS reads where an LDS-DMA piece costs 2-3x the issue cycles (MI355X
