@@ -198,6 +198,11 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_SHORT_SCHED
 #define ATTN_SHORT_SCHED 1
 #endif
+// 512-key (text) cross-attention on 64-key tiles: 73 920 x 512, 1.09 -> 1.035 ms, rel-L2 vs fp64
+// unchanged at 2.81e-3 (profiles/r04_ab_attn_short_nkt2.txt)
+#ifndef ATTN_SHORT_NKT2
+#define ATTN_SHORT_NKT2 1
+#endif
 #ifndef ATTN_FWD_SCHED
 #define ATTN_FWD_SCHED 3
 #endif
@@ -1710,6 +1715,10 @@ int attn_fwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
       hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, true>), grid, dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<false, ATTN_FWD_SCHED, 3, false>), grid, dim3(512), 0, s, a);
+  } else if (ATTN_SHORT_NKT2 && l2q && k_len % 64 == 0 && k_len % 96 != 0) {
+    // cross-attention over the 512 text tokens: 64-key tiles end exactly at k_len (96-key tiles
+    // would spend a sixth tile, two thirds masked, on the last 32 keys)
+    hipLaunchKernelGGL((attn_fwd_kernel<true, ATTN_SHORT_SCHED, 2, true>), grid, dim3(512), 0, s, a);
   } else {
     if (l2q)
       hipLaunchKernelGGL((attn_fwd_kernel<true, ATTN_SHORT_SCHED, 3, true>), grid, dim3(512), 0, s, a);
