@@ -237,6 +237,7 @@ def _l2q(q):
 
 
 @pytest.mark.parametrize("Lq,Lk,H,klen", [(200, 333, 2, 333), (105, 512, 2, 20),
+                                          (300, 512, 2, 512), (700, 1024, 1, 960),
                                           (4200, 4200, 2, 4133), (4111, 5000, 1, 4500)])
 def test_attention_log2_q_vs_oracle(ops, Lq, Lk, H, klen):
     """The q-in-log2-units entries (prfl_attn_fwd_l2q_ws / prfl_attn_bwd_l2q_ws: S accumulators
