@@ -170,7 +170,7 @@ def cpu_baseline():
                 nproc=os.cpu_count())
 
 
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_attn_fwd720_vt.txt")
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_attn_fwd720_vt_final.txt")
 
 
 def pmc_traffic(L):
