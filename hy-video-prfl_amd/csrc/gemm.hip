@@ -680,6 +680,11 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 #ifndef GEMM4_IL
 #define GEMM4_IL 1
 #endif
+// the same placement in the 32x32x16 weight-gradient kernel: dW +5.3-9.5 %, bit-identical
+// (profiles/r04_ab_gemm4x_il.txt)
+#ifndef GEMM4X_IL
+#define GEMM4X_IL 1
+#endif
 // AGPR-accumulator MFMA as inline asm ("+a" keeps hipcc from moving the accumulators to VGPRs)
 __device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
@@ -1036,10 +1041,29 @@ __global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
     // slice j+3 and the reads of fragments c of slice j+1
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
+      const int s = c >> 2, i = c & 3;
+      if (GEMM4X_IL) {       // the four-wave kernel's GEMM4_IL placement: each between two MFMAs
+        auto mf = [&](int jj) {
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+                       : "+a"(acc[i][jj]) : "v"(cb[4 * s + jj]), "v"(ca[c]));
+        };
+        mf(0);
+        piece(c, jd, sd);
+        mf(1);
+        __builtin_amdgcn_sched_barrier(0);
+        na[c] = read_frag32<A_KC>(st, wm * 128 + (c & 3) * 32, c >> 2, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(2);
+        __builtin_amdgcn_sched_barrier(0);
+        nb[c] = read_frag32<B_KC>(st + HALF4, wn * 128 + (c & 3) * 32, c >> 2, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(3);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       piece(c, jd, sd);
       na[c] = read_frag32<A_KC>(st, wm * 128 + (c & 3) * 32, c >> 2, lane);
       nb[c] = read_frag32<B_KC>(st + HALF4, wn * 128 + (c & 3) * 32, c >> 2, lane);
-      const int s = c >> 2, i = c & 3;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)   // D = B . A^T: lanes own consecutive n of one row m
         asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
