@@ -600,6 +600,11 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #ifndef ATTN_BWD_NEGD
 #define ATTN_BWD_NEGD 1
 #endif
+// dK/dV scheduling fences: bit 0 = one every two k-steps of the S / dP chain, bit 1 = one per
+// dV / dK d-tile (3 = both); 0 / 1 / 2 / 3 tie within 0.3 % (profiles/r04_ab_dkdv_sb.txt)
+#ifndef ATTN_DKDV_SB
+#define ATTN_DKDV_SB 3
+#endif
 // (A dQ variant with every LDS fragment read one MFMA step ahead -- the LSE start rebuilt by
 // v_mov to free the registers -- measured bit-identical and no faster: the partner wave already
 // covers the read latency; profiles/r04_attn_dq_pf_ab.txt)
@@ -753,7 +758,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         sacc = mfma32(*(const bf16x8*)(Qs + offB(row, (ks * 2 + hh) * 16)), kf[ks], sacc);
         const bf16x8 vfr = *(const bf16x8*)(Vs + off16(w * 32 + l32, ks * 2 + hh));
         dpt = mfma32(*(const bf16x8*)(Ds + offB(row, (ks * 2 + hh) * 16)), vfr, dpt);
-        if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+        if (ks & 1 & ATTN_DKDV_SB) __builtin_amdgcn_sched_barrier(0);
       }
       // rows q = qb + qt*32 + (r&3) + 8(r>>2) + 4hh
 #pragma unroll
@@ -796,7 +801,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
           dv[dt] = mfma32(dof, pk[s2], dv[dt]);
           dk[dt] = mfma32(qtf, dk8[s2], dk[dt]);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if (ATTN_DKDV_SB & 2) __builtin_amdgcn_sched_barrier(0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
