@@ -605,6 +605,11 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #ifndef ATTN_DKDV_SB
 #define ATTN_DKDV_SB 3
 #endif
+// static priority 1 for waves 4-7 of the backward kernels (MI355X guide, two waves per SIMD,
+// item 4): bit 0 dK/dV, bit 1 dQ
+#ifndef ATTN_BWD_PRIO
+#define ATTN_BWD_PRIO 0
+#endif
 // (A dQ variant with every LDS fragment read one MFMA step ahead -- the LSE start rebuilt by
 // v_mov to free the registers -- measured bit-identical and no faster: the partner wave already
 // covers the read latency; profiles/r04_attn_dq_pf_ab.txt)
@@ -651,6 +656,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const int k0 = kt0 * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (ATTN_BWD_PRIO & 1 && w >= 4) __builtin_amdgcn_s_setprio(1);
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const bf16* Qb = a.Q + b * a.bq + h * HD;
@@ -862,6 +868,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const int q0 = qt0 * 256;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (ATTN_BWD_PRIO & 2 && !ATTN_DQ_STAGGER && w >= 4) __builtin_amdgcn_s_setprio(1);
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const bf16* Qb = a.Q + b * a.bq + h * HD;
