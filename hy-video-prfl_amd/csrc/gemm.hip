@@ -1205,6 +1205,7 @@ extern "C" int prfl_gemm_bf16_tiled(const void* A, int64_t lda, int a_kmajor, co
   GEMM_CASE(1, 0, EPI_DGELU)
   GEMM_CASE(1, 0, EPI_F32)
   GEMM_CASE(0, 0, EPI_F32)
+  GEMM_CASE(0, 0, EPI_BF16)   // both operands MN-major (tools/gemm_run_probe.py: DMA row runs)
   GEMM_CASE(0, 1, EPI_F32)
 #undef GEMM_CASE
   prfl_prof::set_work(2.0 * (double)M * (double)N * (double)K);

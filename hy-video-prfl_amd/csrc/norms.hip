@@ -400,17 +400,3 @@ extern "C" int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const vo
   return 0;
 }
 
-// the round-2 ABI (no out_scale), kept so callers built against it keep working
-extern "C" int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
-                                 float eps, const float* rope_tab, int64_t F, int64_t Hg,
-                                 int64_t Wg, void* out, int64_t ldo, float* rstd, void* stream) {
-  return prfl_rms_rope_fwd_scaled(x, ldx, L, C, w, eps, rope_tab, F, Hg, Wg, out, ldo, rstd, 1.f,
-                                  stream);
-}
-extern "C" int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
-                                 const float* rstd, int64_t L, int64_t C, const float* w,
-                                 const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                                 int64_t lddx, float* part0, void* stream) {
-  return prfl_rms_rope_bwd_scaled(dout, lddo, x, ldx, rstd, L, C, w, rope_tab, F, Hg, Wg, dx, lddx,
-                                  part0, 1.f, stream);
-}

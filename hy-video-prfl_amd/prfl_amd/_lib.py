@@ -52,8 +52,6 @@ SIGNATURES = {
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],
     "prfl_ln_mod_bwd": [P, I64, P, I32, I64, P, P, I64, I64, P, P, P, I64, I32, P, P, P],
     "prfl_norm_rows_per_part": [],
-    "prfl_rms_rope_fwd": [P, I64, I64, I64, P, F32, P, I64, I64, I64, P, I64, P, P],
-    "prfl_rms_rope_bwd": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, P, I64, P, P],
     "prfl_rms_rope_fwd_scaled": [P, I64, I64, I64, P, F32, P, I64, I64, I64, P, I64, P, F32, P],
     "prfl_rms_rope_bwd_scaled": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, P, I64, P, F32,
                                  P],

@@ -15,6 +15,7 @@ What runs where:
 import json
 import math
 import os
+import sys
 
 import torch
 import torch.nn as nn
@@ -271,6 +272,25 @@ class MLPProj(nn.Module):
             return F.layer_norm(h.float(), p[4].normalized_shape, p[4].weight, p[4].bias, p[4].eps)
 
 
+def _refuse_sequence_parallel():
+    """The reference chunks the token sequence across an initialised Ulysses group
+    (`model.py:618-619`, all-to-all `:183-196`, all-gather `:663-676`); this package runs pure
+    data parallelism.  Every shipped training config sets `sp_size: 4`
+    (`configs/train_prfl_t2v_720.yaml:51`): run under it, each rank of a 4-rank group would get
+    the same sample from the sampler (`train_prfl.py:455-464`) and compute the full sequence —
+    4x redundant work with no error.  So an initialised SP state (read from the reference's own
+    `diffusers_lite.utils.parallel_states` if the driver imported it; nothing is imported here)
+    is refused loudly."""
+    ps = sys.modules.get("diffusers_lite.utils.parallel_states")
+    get = getattr(ps, "get_sequence_parallel_state", None)
+    if callable(get) and get():
+        sp = getattr(getattr(ps, "nccl_info", None), "sp_size", "> 1")
+        raise RuntimeError(
+            f"sequence parallelism is initialised (sp_size {sp}), but this WanModel runs pure data "
+            "parallelism: set `sp_size: 1` in the training YAML (INTEGRATION.md, 'Configs').  "
+            "Running on would make every rank of an SP group compute the same sample in full.")
+
+
 class WanModel(nn.Module):
     """model.py:413-729 — Wan2.1 diffusion backbone (t2v / i2v / flf2v)."""
 
@@ -320,7 +340,11 @@ class WanModel(nn.Module):
         projections — QKV, self-attn O, cross-attn q/o, FFN in/out — run as per-row e4m3 operands
         on the block-scaled fp8 MFMA; the backward GEMMs stay bf16 (straight-through).  With
         `attn` the L x L self-attention forward runs on the e4m3 MFMA too (ops.attn_fwd_fp8).
-        Held to an fp32 truth (k x the bf16 path's error), not to the reference (bf16-only)."""
+        Held to an fp32 truth (k x the bf16 path's error), not to the reference (bf16-only).
+        The e4m3 weights are quantised from the fp32 masters: a model whose block weights were
+        stored in bf16 (train.store_frozen_bf16) is refused."""
+        if on and any(p.dtype != torch.float32 for blk in self.blocks for p in blk.parameters()):
+            raise ValueError("set_fp8_gemm: block weights must be fp32 masters (quantised per pass)")
         for blk in self.blocks:
             blk.fp8_gemm = (2 if attn else 1) if on else 0
         return self
@@ -406,6 +430,7 @@ class WanModel(nn.Module):
 
     def forward(self, x, t, context, seq_len, clip_fea=None, y=None, cond_flag=False,
                 output_features=False, selected_layers=[20, 30, 40]):
+        _refuse_sequence_parallel()
         xb, e, e0, ctx, grid_sizes, seq_lens, grids = self._embed(x, t, context, seq_len,
                                                                  clip_fea, y)
         feats = []

@@ -125,10 +125,12 @@ def forward_siamese(model, input1, input2):
 
 
 def _scores(model, model_mode, X):
+    # fp32 scores for BCELoss against fp32 targets: this package's MLP returns bf16 (its Linears
+    # are autocast-style bf16 GEMMs), the reference's fp32 nn.Linear MLP returns fp32
     if model_mode == "clf":
-        return forward_mlp(model, X)
+        return forward_mlp(model, X).float()
     if model_mode == "siamese":                   # X [N, 2, ...]: pair (preferred, other)
-        return forward_siamese(model, X[:, 0], X[:, 1])
+        return forward_siamese(model, X[:, 0], X[:, 1]).float()
     raise ValueError(f"model_mode must be 'clf' or 'siamese', got {model_mode!r}")
 
 
@@ -141,7 +143,13 @@ def train_model(model, device, model_mode, X_train, y_train, X_test, y_test, epo
     reference does); after the epoch the validation BCE is recorded and training stops once it
     exceeds each of the previous `ealry_stopping_patience` values (the reference's spelling of
     the keyword is kept so callers passing it by name still work).  Returns the model (the
-    reference returns None; callers ignore the result)."""
+    reference returns None; callers ignore the result).
+
+    Device: the reference trains an fp32 nn.Linear MLP and runs on the CPU too.  This package's
+    MLP runs its Linears through `prfl::linear_bf16` (bf16 operands, fp32 accumulate, as under
+    the drivers' autocast), a HIP op with no CPU path: `train_model(MLP(...), "cpu", ...)` raises
+    NotImplementedError from the op.  A plain torch classifier trains on any device.  The scores
+    are cast to fp32 before the BCE."""
     model = model.to(device)
     bce = nn.BCELoss()
     opt = torch.optim.Adam(model.parameters(), lr=lr)

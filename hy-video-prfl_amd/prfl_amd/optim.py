@@ -54,8 +54,20 @@ class AdamW:
         self._streams = None
         self._ready = {}            # param -> event (optimizer stream) after its final write
         self._hooks = []
+        # step(zero_grad=True) keeps the gradient buffers (zeroed) where the reference's
+        # optimizer.zero_grad() sets them to None; a parameter whose buffer this optimizer zeroed
+        # and that autograd has not accumulated into since (no gradient in the window) is skipped,
+        # as torch.optim.AdamW skips a None gradient: no weight decay, no moment decay for it
+        self._zeroed = set()
+        self._touched = set()
+        for p in self.params:
+            if p.is_leaf:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._touch))
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                   params=self.params)]
+
+    def _touch(self, p):
+        self._touched.add(p)
 
     def _state(self, p):
         st = self.state.get(p)
@@ -110,6 +122,7 @@ class AdamW:
         for g in groups:
             ps = list(g.parameters())
             self._hooks.append(g.register_forward_pre_hook(lambda m, a, ps=ps: self.wait(ps)))
+        self._attached = True
 
     # ------------------------------------------------------------------ update ------------
     @torch.no_grad()
@@ -121,7 +134,13 @@ class AdamW:
         the old ones on the side stream (which made the caching allocator reserve a second set)."""
         self.step_count += 1
         lr = self.param_groups[0]["lr"]
-        live = [p for p in self.params if p.grad is not None]
+        live = [p for p in self.params
+                if p.grad is not None and (p not in self._zeroed or p in self._touched)]
+        self._touched = set()
+        if zero_grad:
+            self._zeroed.update(live)
+        else:
+            self._zeroed.difference_update(live)
         if not live:
             return
         if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
@@ -135,6 +154,10 @@ class AdamW:
         if self._streams is None:
             self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
         opt, cp = self._streams
+        if self.overlap and zero_grad and not getattr(self, "_attached", False):
+            # the next backward accumulates into buffers this update zeroes on the side stream:
+            # only the forward pre-hooks of attach() order that write after the zeroing
+            raise RuntimeError("AdamW(overlap=True).step(zero_grad=True) needs attach(model) first")
         self.wait(live)                             # a previous step still in flight
         opt.wait_stream(main)                       # grads (clipped) and params are final
         mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
@@ -244,6 +267,8 @@ class AdamW:
     def zero_grad(self, set_to_none=True):
         for p in self.params:
             p.grad = None
+        self._zeroed = set()
+        self._touched = set()
 
     def state_bytes(self):
         return sum(2 * p.numel() * 4 for p in self.state)

@@ -54,8 +54,14 @@ def store_frozen_bf16(model):
     block casts every Linear weight to bf16 before its GEMM anyway (autocast, `model.py`), and a
     bf16 copy made once holds exactly those bits, so outputs are bit-identical while the PRFL
     reward model's 8-block trunk takes 5.6 GB instead of 11.2 at 14B width.  Norm weights,
-    biases and modulation stay fp32 (the kernels read them in fp32).  Refuses trainable weights."""
+    biases and modulation stay fp32 (the kernels read them in fp32).  Refuses trainable weights,
+    and blocks on config C5's fp8 path: there the e4m3 codes and per-row scales are quantised from
+    the fp32 master every pass (block.BF16Weights), and quantising from a bf16 copy instead would
+    change the amax and round twice — the C5 trunk stays fp32.  Swaps `p.data` in
+    place on the caller's model (PRFLTrainer(lrm_weights_bf16=False) leaves it alone)."""
     for blk in model.blocks:
+        if getattr(blk, "fp8_gemm", 0):
+            raise ValueError("store_frozen_bf16: fp8 blocks quantise from the fp32 master")
         for name, p in blk.named_parameters():
             if p.dim() == 2 and name.endswith(".weight"):
                 if p.requires_grad:
@@ -86,8 +92,9 @@ class PRFLTrainer:
                  max_grad_norm=1.0, optimizer_state_on_host=False, optimizer_shard=False,
                  optimizer_overlap=True, lrm_weights_bf16=True):
         self.transformer, self.lrm, self.qa, self.mlp = transformer, lrm, query_attention, mlp
-        if lrm_weights_bf16 and not any(p.requires_grad for p in lrm.parameters()):
-            store_frozen_bf16(lrm)            # frozen reward trunk: bit-identical, half the bytes
+        if (lrm_weights_bf16 and not any(p.requires_grad for p in lrm.parameters())
+                and not any(getattr(b, "fp8_gemm", 0) for b in lrm.blocks)):
+            store_frozen_bf16(lrm)            # frozen bf16 reward trunk: bit-identical, half the bytes
         params = [p for p in transformer.parameters() if p.requires_grad]
         self.params = params
         self.optimizer = AdamW(params, lr=lr, weight_decay=weight_decay,

@@ -75,7 +75,7 @@ int prfl_attn_fwd_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int6
 /* Scratch bytes prfl_attn_fwd_ws needs on the current device (0 = no split for this shape). */
 int64_t prfl_attn_fwd_ws_bytes(int64_t B, int64_t Lq, int64_t Lk, int64_t H, int64_t k_len);
 /* prfl_attn_fwd_ws with q in log2 units, q = q_orig * scale * log2(e) (the fused block's
- * RMSNorm+RoPE writes it so, prfl_rms_rope_fwd out_scale): the S accumulators start at the running
+ * RMSNorm+RoPE writes it so, prfl_rms_rope_fwd_scaled out_scale): the S accumulators start at the running
  * row max and P = exp2(S) takes one v_exp per score.  o / lse2 are those of
  * prfl_attn_fwd_ws(q_orig, ..., scale); same scratch. */
 int prfl_attn_fwd_l2q_ws(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t ldk,
@@ -200,16 +200,12 @@ int prfl_norm_rows_per_part(void);
  * model.py:61-103; rope_tab = fp32 (cos,sin) [1024][64] of the complex freqs of model.py:521-526,
  * grid (F,Hg,Wg); rows >= F*Hg*Wg are not rotated; rope_tab == NULL -> no RoPE).
  *   out = bf16(rope(bf16(x * rsqrt(mean(x^2)+eps)) * w) * out_scale)
- * prfl_rms_rope_fwd / _bwd are the reference's norm_q / norm_k (out_scale 1).  The _scaled forms
- * (added in round 3) multiply the output by out_scale: softmax_scale * log2(e) yields the q operand
- * of the *_l2q attention entries; the backward scales the incoming gradient by out_scale. */
-int prfl_rms_rope_fwd(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w, float eps,
-                      const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* out,
-                      int64_t ldo, float* rstd, void* stream);
-int prfl_rms_rope_bwd(const void* dout, int64_t lddo, const void* x, int64_t ldx,
-                      const float* rstd, int64_t L, int64_t C, const float* w,
-                      const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
-                      int64_t lddx, float* part0, void* stream);
+ * out_scale 1 is the reference's norm_q / norm_k; softmax_scale * log2(e) yields the q operand of
+ * the *_l2q attention entries; the backward scales the incoming gradient by out_scale.
+ * There is deliberately no unsuffixed prfl_rms_rope_fwd / _bwd: that name carried two different
+ * signatures (round 2 without out_scale, round 3 with it), and a float argument dropped from a
+ * SysV signature still links, so a stale caller would run with the wrong scale.  Removing the
+ * name (round 5) makes such a caller fail to resolve instead (ABI history). */
 int prfl_rms_rope_fwd_scaled(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
                              float eps, const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg,
                              void* out, int64_t ldo, float* rstd, float out_scale, void* stream);

@@ -216,3 +216,144 @@ def test_nan_loss_skip_is_agreed_across_ranks_world2():
     (_, r0), (_, r1) = res
     assert r0[0] and r1[0]
     assert r0[1] == 1e6 and r1[1] == 0.25
+
+
+# ---- world 4: the trainer's whole collective schedule, recorded per rank ---------------------
+# RCCL (like NCCL) needs every rank to issue the same collectives in the same order: the
+# GradReducer's all-reduces (post-accumulate hooks, in autograd's order, then the coalesced small
+# tensors at end()), the guard's MAX flag, the loss averages, mid_timestep's broadcast and the
+# ZeRO-1 per-tensor broadcasts from the optimizer step.  The toy modules below stand in for the
+# HIP-backed WanModel (which has no CPU path) behind the same call signature; the compute ops the
+# trainer calls directly (UniPC update, clip, AdamW) are swapped for their torch restatements.
+
+class _ToyWan(torch.nn.Module):
+    """WanModel's forward signature over a [16, F, H, W] latent; blocks of mixed sizes so the
+    GradReducer takes both its per-tensor and its coalesced path."""
+
+    def __init__(self, dim=32, n_blocks=3, head=True):
+        super().__init__()
+        self.patch = torch.nn.Linear(16, dim)
+        self.text = torch.nn.Linear(4096, dim)
+        self.time = torch.nn.Parameter(torch.zeros(dim))
+        self.blocks = torch.nn.ModuleList(
+            [torch.nn.Sequential(torch.nn.Linear(dim, 4 * dim), torch.nn.Tanh(),
+                                 torch.nn.Linear(4 * dim, dim)) for _ in range(n_blocks)])
+        self.head = torch.nn.Linear(dim, 16) if head else None
+
+    def forward(self, x, t, context, seq_len, clip_fea=None, y=None, output_features=False,
+                selected_layers=(2,)):
+        u = x[0]
+        c, f, h, w = u.shape
+        tok = u.reshape(c, -1).t().float()
+        hcur = self.patch(tok) + self.text(context[0].float().mean(0)) + \
+            self.time * (t.float().reshape(()) / 1000)
+        feats = []
+        for i, b in enumerate(self.blocks):
+            hcur = hcur + b(hcur)
+            if output_features and i + 1 in selected_layers:
+                feats.append(hcur.unsqueeze(0))
+        if output_features:
+            return feats
+        return [self.head(hcur).t().reshape(c, f, h, w).to(u.dtype)]
+
+
+class _ToyQA(torch.nn.Module):
+    def __init__(self, dim=32):
+        super().__init__()
+        self.q = torch.nn.Linear(dim, dim)
+
+    def forward(self, feats):
+        return self.q(feats.mean(dim=(0, 2)))
+
+
+def _record_collectives(log):
+    real = {n: getattr(dist, n) for n in ("all_reduce", "broadcast")}
+
+    def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
+        log.append(("all_reduce", tuple(t.shape), str(t.dtype), str(op)))
+        return real["all_reduce"](t, op=op, group=group, async_op=async_op)
+
+    def broadcast(t, src=0, group=None, async_op=False):
+        log.append(("broadcast", tuple(t.shape), str(t.dtype), int(src)))
+        return real["broadcast"](t, src=src, group=group, async_op=async_op)
+    dist.all_reduce, dist.broadcast = all_reduce, broadcast
+    return real
+
+
+def _trainer_worker(rank, world, port, out_q):
+    import random
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import wan_oracle as O
+    from prfl_amd import optim
+    from prfl_amd.schedulers import FlowUniPCMultistepScheduler
+    from prfl_amd.train import PRFLTrainer
+    FlowUniPCMultistepScheduler._update = staticmethod(O.unipc_update)
+    optim.ops.adamw_ = _adamw_ref
+    optim.ops.sumsq_ = lambda g, ss: ss.add_(g.double().square().sum().float())
+    optim.ops.scale_ = lambda g, coef: g.mul_(coef)
+    torch.manual_seed(0)                               # identical replicas on every rank
+    gen, lrm = _ToyWan(), _ToyWan(n_blocks=2, head=False)
+    lrm.requires_grad_(False)
+    qa, mlp = _ToyQA(), torch.nn.Linear(32, 1)
+    qa.requires_grad_(False)
+    mlp.requires_grad_(False)
+    tr = PRFLTrainer(gen, lrm, qa, mlp, lr=1e-3, grad_accum=2.0, inference_steps=6,
+                     feature_layer=(2,), optimizer_shard=True, optimizer_overlap=True,
+                     lrm_weights_bf16=False)
+    tr.reducer.small_numel = 600                       # block weights reduce alone, biases coalesce
+    log = []
+    real = _record_collectives(log)
+    random.seed(1000 + rank)                           # each rank draws its own mid: rank 0's wins
+    g = torch.Generator().manual_seed(7 + rank)        # distinct data per rank
+    latents = torch.randn(1, 16, 2, 4, 4, generator=g)
+    text = torch.randn(1, 5, 4096, generator=g)
+    mids = []
+    for step in range(4):                              # two iterations, each SFT + reward; GA 2
+        tr.sft_step(step, latents, text, 32, generator=g)
+        mids.append(tr.reward_step(step, latents, text, 32, generator=g)["mid"])
+    dist.all_reduce, dist.broadcast = real["all_reduce"], real["broadcast"]
+    loads = [0] * world
+    for p, r in tr.optimizer.owner.items():
+        loads[r] += p.numel()
+    out_q.put((rank, log, mids, loads, max(p.numel() for p in tr.params),
+               [p.detach().numpy().copy() for p in gen.parameters()], len(tr.optimizer.state)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_prfl_trainer_collective_sequence_identical_world4():
+    """four ranks run two PRFL iterations (SFT + reward, gradient accumulation 2,
+    ZeRO-1 with overlap=True) through PRFLTrainer; every rank must issue the identical collective
+    sequence (op, shape, dtype, reduce-op / root), the replicas must stay identical, rank 0's
+    mid_timestep must reach every rank, and the ZeRO-1 ownership must be size-balanced."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 4
+    port = 33500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([_to_torch(q.get(timeout=300)) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    logs = [r[1] for r in res]
+    assert len(logs[0]) > 40
+    for r in range(1, world):
+        assert logs[r] == logs[0], f"rank {r} diverges at collective " \
+            f"{next(i for i, (a, b) in enumerate(zip(logs[r], logs[0])) if a != b)}"
+    kinds = {e[0] for e in logs[0]}
+    assert kinds == {"all_reduce", "broadcast"}
+    # one ZeRO-1 broadcast per trainable tensor per optimizer step (steps 1 and 3: two per step)
+    n_params = len(res[0][5])
+    roots = [e[3] for e in logs[0] if e[0] == "broadcast" and e[1] != (1,)]
+    assert len(roots) == 2 * 2 * n_params and set(roots) == set(range(world))
+    mids = [r[2] for r in res]
+    assert all(m == mids[0] for m in mids)
+    loads, biggest = res[0][3], res[0][4]
+    assert max(loads) - min(loads) <= biggest, loads
+    assert sum(r[6] for r in res) == n_params         # each tensor's moments on exactly one rank
+    for r in range(1, world):
+        for a, b in zip(res[r][5], res[0][5]):
+            assert torch.equal(a, b)

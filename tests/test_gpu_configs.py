@@ -240,3 +240,62 @@ def test_c5_prfl_i2v_720_fp8_real_width():
     """C5 `train_prfl_i2v_720`: the I2V model (36 input channels, 257 CLIP tokens of image
     cross-attention) at 720p x 81f with the fp8 path on (set_fp8_gemm(True, attn=True))."""
     _prfl("i2v", 21, 88, 160, fp8=True, big=True)
+
+
+def test_c3_block_gradients_at_real_geometry():
+    """gradients at real geometry.  One 14B block (C = 5120, 40 heads,
+    F = 13 824) at config C3's 480p x 81f geometry (grid 21 x 30 x 52, L = 32 760): the fused HIP
+    block's output, input gradient and projection-weight gradients (self_attn.q — through the
+    self-attention backward — and ffn.2) vs a GPU fp32 checker (`tests/gpu_block_checker.py`:
+    the oracle's block with a query-chunked FA2 attention).  The checker is first held to the CPU
+    oracle at L = 4 200 in this test (same block, same cast points; <= 5e-3), then used at
+    L = 32 760 with the block tolerances (output <= 1e-2, gradients <= 3e-2)."""
+    import gpu_block_checker as GC
+    from shapes import block_shapes, seeded_params
+    from prfl_amd import block as B
+    from prfl_amd import ops
+    torch.set_num_threads(16)
+    P = seeded_params(block_shapes("blocks.0.", 5120, 13824, False), prefix="c3grad.")
+    names = ("self_attn.q.weight", "self_attn.o.weight", "ffn.2.weight", "ffn.0.bias")
+    # (1) the checker vs the CPU oracle at L = 4 200
+    grid, L = (3, 35, 40), 4200
+    g = torch.Generator().manual_seed(33)
+    x = torch.randn(1, L, 5120, generator=g)
+    e = torch.randn(1, 6, 5120, generator=g) * 0.1
+    ctx = torch.randn(1, 512, 5120, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, 5120, generator=g)
+    co, cdx, cG = GC.block_grads(P, "blocks.0.", x, e, ctx, grid, L, 40, up)
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    xr = x.clone().requires_grad_(True)
+    ref = O.block_forward(Pr, "blocks.0.", xr, e, torch.tensor([grid]), O.rope_freqs(128),
+                          ctx.float(), 40, seq_len=L)
+    (ref * up).sum().backward()
+    rep = {"L4200 checker out": rel(co, ref), "L4200 checker dx": rel(cdx, xr.grad)}
+    for n in names:
+        rep["L4200 checker " + n] = rel(cG[n], Pr["blocks.0." + n].grad)
+    assert all(v <= 5e-3 for v in rep.values()), rep
+    del Pr, xr, ref
+    # (2) the HIP block vs the checker at L = 32 760 (config C3's geometry)
+    grid = (21, 30, 52)
+    L = 21 * 30 * 52
+    g = torch.Generator().manual_seed(32760)
+    x = torch.randn(1, L, 5120, generator=g)
+    e = torch.randn(1, 6, 5120, generator=g) * 0.1
+    ctx = torch.randn(1, 512, 5120, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, 5120, generator=g)
+    Pd = {n: P["blocks.0." + n].to(DEV).requires_grad_(True) for n in B.param_names(False)}
+    xd = x.to(DEV).requires_grad_(True)
+    meta = B.Meta(40, [grid], [L], ops.rope_table(O.rope_freqs(128), DEV), False)
+    out = B.block_apply(Pd, xd, (P["blocks.0.modulation"] + e).to(DEV), ctx.to(DEV), meta)
+    (out * up.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    ours = (out.detach().cpu(), xd.grad.cpu(), {n: Pd[n].grad.cpu() for n in names})
+    del out, xd, Pd
+    torch.cuda.empty_cache()
+    co, cdx, cG = GC.block_grads(P, "blocks.0.", x, e, ctx, grid, L, 40, up)
+    rep.update({"L32760 out": rel(ours[0], co), "L32760 dx": rel(ours[1], cdx)})
+    for n in names:
+        rep["L32760 " + n] = rel(ours[2][n], cG[n])
+    print("C3 block gradients", rep)
+    assert rep["L32760 out"] < 1e-2, rep
+    assert all(v < 3e-2 for k, v in rep.items() if k.startswith("L32760")), rep

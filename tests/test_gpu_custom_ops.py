@@ -199,3 +199,19 @@ def test_query_pool_vs_reference(cops, N, L, E, H):
     assert rel(qg.grad, qr.grad) < 2e-2
     assert rel(kvg.grad[:, :, :E], kvr.grad[:, :, :E]) < 2e-2
     assert rel(kvg.grad[:, :, E:], kvr.grad[:, :, E:]) < 2e-2
+
+
+def test_train_model_on_the_reward_mlp():
+    """network.train_model on this package's reward MLP (bf16 GEMMs on the HIP op): the scores
+    reach BCELoss in fp32 (the reference's fp32 nn.Linear MLP gives fp32), and it trains."""
+    from prfl_amd.network import MLP, _scores, train_model
+    torch.manual_seed(0)
+    X = torch.randn(512, 64, device=DEV)
+    y = (X[:, :1] > 0).float()
+    m = MLP(64).to(DEV)
+    assert _scores(m, "clf", X).dtype == torch.float32
+    bce = torch.nn.functional.binary_cross_entropy
+    before = bce(_scores(m, "clf", X), y).item()
+    train_model(m, DEV, "clf", X, y, X, y, epochs=30, lr=3e-3, batch_size=128)
+    after = bce(_scores(m, "clf", X), y).item()
+    assert after < 0.7 * before, (before, after)

@@ -412,3 +412,116 @@ def test_attn_fp8_vs_fp64_truth(L, H):
     print(f"attn C5 vs truth {e8:.3e}, bf16 vs truth {e16:.3e}, ratio {e8 / e16:.2f}")
     assert e8 <= 24 * e16, (e8, e16)
     assert e8 < 6e-2
+
+
+def test_c5_reward_gradient_direction_vs_bf16_and_truth():
+    """what config C5's fp8 path does to the gradient PRFL trains on.  The
+    generator piece of the reward backward (`train_prfl.py:703-830`: one grad-enabled generator
+    step at t_mid, then the differentiable UniPC step, with a fixed upstream d(stepped)) at real
+    width (I2V, C = 5120, 40 heads, F = 13 824, 2 blocks + embeddings + head, 257 CLIP tokens) and
+    L = 4 200 (latent [16, 3, 70, 80]), mid_timestep 0, on three paths with the same weights and
+    inputs: the bf16 path, the fp8 path (set_fp8_gemm(True, attn=True): e4m3 projections, int8 /
+    e4m3 self-attention forward, bf16 backward), and the oracle's fp32 TRUTH (wan_oracle's model
+    with every cast point removed, run on the GPU by tests/gpu_block_checker.py, + the oracle's
+    UniPC step).  Per parameter: rel-L2 and cosine of the fp8 gradient vs the truth and vs the
+    bf16 gradient; the whole gradient's cosine.  Bounds: see the asserts."""
+    import math
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gpu_block_checker as GC
+    from tolerance import key_path_scale
+    from oracle import wan_oracle as O
+    from prfl_amd.model import WanModel
+    from prfl_amd.schedulers import FlowUniPCMultistepScheduler
+    from prfl_amd.train import batch2list, list2batch
+    torch.manual_seed(5)
+    with torch.device(DEV):
+        gen = WanModel(model_type="i2v", in_dim=36, num_layers=2, dim=5120, ffn_dim=13824,
+                       freq_dim=256, text_dim=4096, out_dim=16, num_heads=40)
+        torch.nn.init.normal_(gen.head.head.weight, std=0.02)   # random-init trap (SURVEY §7.2)
+    Fl, Hl, Wl = 3, 70, 80
+    L = Fl * (Hl // 2) * (Wl // 2)
+    g = torch.Generator(device=DEV).manual_seed(4200)
+    lat = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=DEV).to(torch.bfloat16)
+    text = (0.08 * torch.randn(1, 126, 4096, generator=g, device=DEV)).to(torch.bfloat16)
+    clip = torch.randn(1, 257, 1280, generator=g, device=DEV).to(torch.bfloat16)
+    cond = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=DEV).to(torch.bfloat16)
+    mask = torch.zeros(1, 4, Fl, Hl, Wl, device=DEV, dtype=torch.bfloat16)
+    mask[:, :, :1] = 1
+    cond = torch.cat([mask, cond], dim=1)
+    up = torch.randn(1, 16, Fl, Hl, Wl, generator=g, device=DEV)
+    names = [n for n, _ in gen.named_parameters()]
+
+    def ours(fp8):
+        gen.set_fp8_gemm(fp8, attn=fp8)
+        for p in gen.parameters():
+            p.grad = None
+        sch = FlowUniPCMultistepScheduler(num_train_timesteps=1000, shift=1,
+                                          use_dynamic_shifting=False)
+        sch.set_timesteps(num_inference_steps=40, device=DEV, shift=5.0)
+        t = sch.timesteps[0]
+        npred = list2batch(gen(x=batch2list(lat), t=t.reshape(1), context=batch2list(text),
+                               seq_len=L, clip_fea=clip, y=batch2list(cond)))
+        stepped = sch.step(npred, t, lat, return_dict=False)[0]
+        (stepped.float() * up).sum().backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().float().cpu() for n, p in gen.named_parameters()}, int(t)
+
+    g16, t0 = ours(False)
+    g8, _ = ours(True)
+    gen.set_fp8_gemm(False)
+    # the fp32 truth: the oracle's model on the GPU with every bf16 cast point removed
+    cfg = dict(dim=5120, num_heads=40, model_type="i2v", freq_dim=256, text_len=512, out_dim=16,
+               num_layers=2)
+    Pd = {n: p.detach().float().clone().requires_grad_(True) for n, p in gen.named_parameters()}
+    saved = O.bf
+    O.bf = lambda t: t
+    try:
+        with GC.oracle_on(DEV):
+            out = O.model_forward(Pd, cfg, [lat[0].float()], torch.tensor([t0], device=DEV),
+                                  [text[0].float()], L, clip_fea=clip.float(),
+                                  y_list=[cond[0].float()])
+            sch = O.UniPCOracle(40, 5.0)
+            stepped = sch.step(out[0], t0, lat[0].float())
+            (stepped * up[0]).sum().backward()
+    finally:
+        O.bf = saved
+    torch.cuda.synchronize()
+    gt = {n: Pd[n].grad.detach().float().cpu() for n in names}
+    del Pd, out, stepped
+
+    def cos(a, b):
+        a, b = a.double().flatten(), b.double().flatten()
+        return (a @ b / (a.norm() * b.norm()).clamp_min(1e-300)).item()
+    gnp = {"grad/" + n: v.numpy() for n, v in gt.items()}
+    rows = []
+    for n in names:
+        if key_path_scale(gnp, n) is not None or gt[n].norm() == 0:
+            continue                       # cancellation-dominated key-side directions
+        rows.append((n, rel(g8[n], gt[n]), rel(g16[n], gt[n]), cos(g8[n], gt[n]),
+                     cos(g16[n], gt[n]), cos(g8[n], g16[n])))
+    cat = lambda d: torch.cat([d[n].flatten() for n in names])  # noqa: E731
+    whole = {"fp8 vs truth": cos(cat(g8), cat(gt)), "bf16 vs truth": cos(cat(g16), cat(gt)),
+             "fp8 vs bf16": cos(cat(g8), cat(g16)),
+             "fp8 rel vs truth": rel(cat(g8), cat(gt)), "bf16 rel vs truth": rel(cat(g16), cat(gt))}
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+    print("whole-gradient", {k: round(v, 5) for k, v in whole.items()})
+    print("per-parameter (%d): fp8 rel vs truth median %.4f max %.4f | bf16 median %.4f max %.4f | "
+          "fp8 cos vs truth min %.5f | fp8 cos vs bf16 min %.5f" % (
+              len(rows), med([r[1] for r in rows]), max(r[1] for r in rows),
+              med([r[2] for r in rows]), max(r[2] for r in rows), min(r[3] for r in rows),
+              min(r[5] for r in rows)))
+    for r in sorted(rows, key=lambda r: -r[1])[:12]:
+        print("  %-40s fp8 rel %.4f (bf16 %.4f)  cos fp8/truth %.5f  bf16/truth %.5f  fp8/bf16 %.5f"
+              % r)
+    assert all(math.isfinite(v) for r in rows for v in r[1:])
+    # bf16 path: the parity bar of every other gradient test
+    assert whole["bf16 rel vs truth"] < 3e-2 and whole["bf16 vs truth"] > 0.999, whole
+    # fp8 path: the C5 rule of test_block_fp8_vs_fp32_truth on the whole gradient (<= 16 x the
+    # bf16 path's error and <= 1e-1) and the direction kept: cosine to the truth >= 0.99
+    assert whole["fp8 rel vs truth"] <= 16 * whole["bf16 rel vs truth"], whole
+    assert whole["fp8 rel vs truth"] <= 1e-1 and whole["fp8 vs truth"] >= 0.99, whole
+    for n, e8, e16, c8, c16, c816 in rows:
+        assert e8 <= max(16 * e16, 2e-2) and c8 >= 0.95, (n, e8, e16, c8)

@@ -745,27 +745,34 @@ def test_colsum_reduce(ops, P, N):
 def test_adamw_zero_grad_in_step_is_bit_exact(ops):
     """step(zero_grad=True) (the update kernel zeroes each gradient once read, buffers kept) ==
     step() + zero_grad(): identical parameters over several steps with the next gradient
-    accumulated into the zeroed buffer, overlapped, with device and host-streamed moments; the
-    gradient tensors are the same storage throughout."""
+    accumulated by autograd into the zeroed buffer behind attach()'s forward pre-hook, overlapped,
+    with device and host-streamed moments; the gradient tensors are the same storage throughout."""
     from prfl_amd.optim import AdamW
     g = torch.Generator().manual_seed(8)
     shapes = [(3000,), (257, 33), (5,), (1024, 64)]
     base = [torch.randn(s, generator=g) for s in shapes]
     grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(4)]
+
+    class Holder(torch.nn.Module):
+        def __init__(self, ts):
+            super().__init__()
+            self.ps = torch.nn.ParameterList([torch.nn.Parameter(t) for t in ts])
+
+        def forward(self, gs):                     # d/dp sum(p * g) = g, accumulated into .grad
+            return sum((p * gr).sum() for p, gr in zip(self.ps, gs))
+
     for host in (False, True):
         a = [x.clone().to(DEV).requires_grad_(True) for x in base]
-        b = [x.clone().to(DEV).requires_grad_(True) for x in base]
+        hb = Holder([x.clone().to(DEV) for x in base])
+        b = list(hb.ps)
         oa = AdamW(a, lr=1e-2, state_on_host=host)
         ob = AdamW(b, lr=1e-2, state_on_host=host, overlap=True, ring_slots=2)
+        ob.attach(hb, groups=[])                   # the forward waits for every pending update
         ptrs = None
         for gs in grads:
-            for pa, pb, gr in zip(a, b, gs):
+            for pa, gr in zip(a, gs):
                 pa.grad = gr.to(DEV)
-                if pb.grad is None:
-                    pb.grad = gr.to(DEV)
-                else:
-                    ob.wait([pb])
-                    pb.grad += gr.to(DEV)              # AccumulateGrad into the zeroed buffer
+            hb([gr.to(DEV) for gr in gs]).backward()
             oa.step()
             oa.zero_grad()
             ob.step(zero_grad=True)
@@ -777,3 +784,55 @@ def test_adamw_zero_grad_in_step_is_bit_exact(ops):
         ob.synchronize()
         for pa, pb in zip(a, b):
             assert torch.equal(pa, pb), host
+
+
+def test_adamw_zero_grad_skips_untouched_like_set_to_none(ops):
+    """The reference's optimizer.zero_grad() sets gradients to None, and torch.optim.AdamW then
+    skips a parameter that gets no gradient in the next window (no weight decay, no moment
+    decay).  step(zero_grad=True) keeps the buffers zeroed instead; a buffer it zeroed that
+    autograd has not accumulated into since is skipped the same way.  A toy model
+    whose block 1 is bypassed in every other window, trained with the overlapped, hook-ordered
+    update (attach), vs torch.optim.AdamW(foreach=False) + zero_grad(set_to_none=True)."""
+    from prfl_amd.optim import AdamW
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Linear(16, 64)
+            self.blocks = torch.nn.ModuleList([torch.nn.Linear(64, 64) for _ in range(3)])
+            self.head = torch.nn.Linear(64, 3)
+
+        def forward(self, x, skip=()):
+            x = self.emb(x)
+            for i, b in enumerate(self.blocks):
+                if i not in skip:
+                    x = torch.tanh(b(x))
+            return self.head(x)
+
+    torch.manual_seed(0)
+    ref, ours = Toy().to(DEV), Toy().to(DEV)
+    ours.load_state_dict(ref.state_dict())
+    x = torch.randn(32, 16, device=DEV)
+    topt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.01, foreach=False)
+    oopt = AdamW(list(ours.parameters()), lr=1e-2, overlap=True)
+    oopt.attach(ours)
+    for it in range(6):
+        skip = (1,) if it % 2 else ()
+        ref(x, skip).square().mean().backward()
+        ours(x, skip).square().mean().backward()
+        topt.step()
+        topt.zero_grad(set_to_none=True)
+        oopt.step(zero_grad=True)
+    oopt.synchronize()
+    for (n, pr), po in zip(ref.named_parameters(), ours.parameters()):
+        assert (pr - po).abs().max().item() <= 1e-6, n
+    # without the skip, the bypassed block would have decayed (weight decay + moments)
+    assert oopt.step_count == 6
+
+
+def test_adamw_overlap_zero_grad_requires_attach(ops):
+    from prfl_amd.optim import AdamW
+    p = torch.zeros(8, device=DEV, requires_grad=True)
+    p.grad = torch.ones(8, device=DEV)
+    with pytest.raises(RuntimeError, match="attach"):
+        AdamW([p], overlap=True).step(zero_grad=True)

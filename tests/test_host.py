@@ -28,6 +28,18 @@ def test_abi_library_exports_header():
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
 
 
+def test_abi_stale_rms_rope_names_removed():
+    """The unsuffixed prfl_rms_rope_fwd / _bwd carried two signatures (round 2 without out_scale,
+    round 3 with it); a caller built against either must fail to resolve, not run with a silently
+    dropped scale (ABI history)."""
+    from prfl_amd import _lib
+    lib = _lib.load()
+    for s in ("prfl_rms_rope_fwd", "prfl_rms_rope_bwd"):
+        assert not hasattr(lib, s), s
+        assert s not in declared_symbols()
+    assert hasattr(lib, "prfl_rms_rope_fwd_scaled") and hasattr(lib, "prfl_rms_rope_bwd_scaled")
+
+
 def test_no_cpu_fallback():
     from prfl_amd import ops
     x = torch.zeros(8, 64, dtype=torch.bfloat16)
@@ -135,6 +147,28 @@ def test_train_model_and_save_model(tmp_path):
         assert all(torch.equal(sd[k], v) for k, v in m.state_dict().items())
     with pytest.raises(ValueError):
         train_model(m, "cpu", "ranking", X, y, X, y, epochs=1)
+    # this package's reward MLP is a bf16 GEMM on the HIP op: no CPU path, documented
+    from prfl_amd.network import MLP
+    with pytest.raises(NotImplementedError):
+        train_model(MLP(8), "cpu", "clf", X, y, X, y, epochs=1)
+
+
+def test_fp8_path_keeps_fp32_masters():
+    """C5 quantises its e4m3 weights from the fp32 masters every pass: a bf16-stored trunk is
+    refused in either order, and the PRFL trainer keeps an fp8 trunk in fp32."""
+    from prfl_amd.model import WanModel
+    from prfl_amd.train import store_frozen_bf16
+    kw = dict(dim=64, ffn_dim=128, num_heads=2, num_layers=1, in_dim=16)
+    m = WanModel(**kw).set_fp8_gemm(True)
+    m.requires_grad_(False)
+    with pytest.raises(ValueError, match="fp8"):
+        store_frozen_bf16(m)
+    m2 = WanModel(**kw)
+    m2.requires_grad_(False)
+    store_frozen_bf16(m2)
+    assert m2.blocks[0].ffn[0].weight.dtype == torch.bfloat16
+    with pytest.raises(ValueError, match="fp32"):
+        m2.set_fp8_gemm(True)
 
 
 def test_unipc_product_vs_reference(golden):
@@ -253,3 +287,27 @@ def test_loss_guard_matches_reference_semantics():
     ok = guard_loss(y * 2)
     ok.backward()
     assert float(ok) == float(torch.tensor(0.3) * 2) and float(y.grad) == 2.0
+
+
+@pytest.mark.parametrize("state", [True, False])
+def test_forward_refuses_initialised_sequence_parallel(monkeypatch, state):
+    """with the reference's `parallel_states` reporting an initialised SP group
+    (as every shipped YAML's `sp_size: 4` leaves it), WanModel.forward raises and names the fix,
+    instead of running 4x redundant work; with SP off it proceeds (to the HIP op, which has no
+    CPU path here)."""
+    import sys
+    import types
+    from prfl_amd.model import WanModel
+    ps = types.ModuleType("diffusers_lite.utils.parallel_states")
+    ps.get_sequence_parallel_state = lambda: state
+    ps.nccl_info = types.SimpleNamespace(sp_size=4 if state else 1)
+    monkeypatch.setitem(sys.modules, "diffusers_lite.utils.parallel_states", ps)
+    m = WanModel(dim=64, ffn_dim=128, num_heads=2, num_layers=1, in_dim=16)
+    x = [torch.randn(16, 1, 4, 4)]
+    ctx = [torch.randn(8, 4096)]
+    if state:
+        with pytest.raises(RuntimeError, match="sp_size: 1"):
+            m(x, torch.tensor([500]), ctx, seq_len=4)
+    else:
+        with pytest.raises(NotImplementedError):
+            m(x, torch.tensor([500]), ctx, seq_len=4)

@@ -176,3 +176,33 @@ def test_oracle_row_subset_and_chunked_attention_match_full():
         a = O.attention(q, k, v, k_len=50, q_chunk=16)
     b = O._FlashAttention.apply(q, k, v, 50, 128 ** -0.5)
     assert (a - b).abs().max().item() <= 2 ** -8 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("i2v", [False, True])
+def test_gpu_block_checker_matches_oracle_on_cpu(i2v):
+    """tests/gpu_block_checker.py (the oracle's block with a query-chunked FA2 attention, the
+    checker of test_gpu_configs.py's real-geometry gradient test) run on the CPU at toy width
+    equals the oracle's own autograd: output exactly, input gradient and every parameter gradient
+    to fp32 rounding (the key bias, cancellation-dominated, to 5e-3)."""
+    import gpu_block_checker as GC
+    from shapes import block_shapes, seeded_params
+    P = seeded_params(block_shapes("blocks.0.", 256, 512, i2v), prefix="chk.")
+    L, grid = 105, (3, 5, 7)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1, L, 256, generator=g)
+    e = torch.randn(1, 6, 256, generator=g) * 0.1
+    ctx = torch.randn(1, 769 if i2v else 512, 256, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, 256, generator=g)
+    co, cdx, cG = GC.block_grads(P, "blocks.0.", x, e, ctx, grid, L, 2, up, device="cpu", i2v=i2v,
+                                 chunk=32)
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    xr = x.clone().requires_grad_(True)
+    ref = O.block_forward(Pr, "blocks.0.", xr, e, torch.tensor([grid]), O.rope_freqs(128),
+                          ctx.float(), 2, seq_len=L, i2v=i2v)
+    (ref * up).sum().backward()
+    r = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert torch.equal(co, ref.detach())
+    assert r(cdx, xr.grad) < 1e-4
+    for k, v in Pr.items():
+        if v.grad is not None:
+            assert r(cG[k[len("blocks.0."):]], v.grad) < 5e-3, k

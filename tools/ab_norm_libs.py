@@ -1,6 +1,6 @@
 """Dev A/B of builds of the RMSNorm+RoPE forward in ONE process, interleaved:
     python tools/ab_norm_libs.py <lib1.so> <lib2.so> ... [--reps 10]
-prfl_rms_rope_fwd at the 720p self-attention q shape (L = 73 920 rows of a [L, 3C] QKV output,
+prfl_rms_rope_fwd_scaled at the 720p self-attention q shape (L = 73 920 rows of a [L, 3C] QKV output,
 C = 5120, 3-D RoPE over the 21 x 44 x 80 grid, out_scale = scale * log2 e), HIP events on the
 launch stream; prints medians, GB/s (read 2 B + write 2 B per element) and the largest output
 difference vs the first build in bf16 ulps."""
@@ -27,7 +27,7 @@ def main():
     libs = []
     for p in a.libs:
         lib = ctypes.CDLL(os.path.abspath(p))
-        lib.prfl_rms_rope_fwd.argtypes, lib.prfl_rms_rope_fwd.restype = SIG, ctypes.c_int
+        lib.prfl_rms_rope_fwd_scaled.argtypes, lib.prfl_rms_rope_fwd_scaled.restype = SIG, ctypes.c_int
         libs.append(lib)
     from prfl_amd import ops
     from prfl_amd.model import _rope_table, rope_params
@@ -50,7 +50,7 @@ def main():
         for i, lib in enumerate(libs):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = lib.prfl_rms_rope_fwd(qkv.data_ptr(), 3 * C, L, C, w.data_ptr(), 1e-6, tab.data_ptr(),
+            rc = lib.prfl_rms_rope_fwd_scaled(qkv.data_ptr(), 3 * C, L, C, w.data_ptr(), 1e-6, tab.data_ptr(),
                                        F, Hg, Wg, outs[i].data_ptr(), C, rstd[i].data_ptr(), sc, st)
             e1.record()
             torch.cuda.synchronize()

@@ -124,6 +124,35 @@ elif which == "gemmepi":
             dt = time.time() - t0
             print(f"gemm {name} {L}x{N}x{K} {dt*1e3:.2f} ms  {2*L*N*K/dt/1e12:.0f} TF/s", flush=True)
         del x, w, aux, kw
+elif which == "gemm720t":
+    # the SHIPPED GEMMs of a 720p block, one dispatch each per rep, for PMC runs: forward on the
+    # W^T image (gemm4w_kernel<true,false,EPI>: QKV +bias, o-proj / FFN-down gated residual,
+    # FFN-up GELU), dX (gemm4w_kernel<true,false,EPI_BF16>), dW (gemm4x_kernel<false,false,F32>)
+    for name, N, K, epi in (("qkv", 3 * C, C, ops.EPI_BF16), ("o_resid", C, C, ops.EPI_RESID),
+                            ("ffn1_gelu", F, C, ops.EPI_GELU), ("ffn2_resid", C, F, ops.EPI_RESID)):
+        x = torch.randn(L, K, device=dev, generator=g).to(torch.bfloat16)
+        w32 = torch.randn(N, K, device=dev, generator=g) * 0.02
+        wt, w = ops.cast_bf16_t(w32), w32.to(torch.bfloat16)
+        bias = (0.02 * torch.randn(N, device=dev, generator=g)).to(torch.bfloat16)
+        aux = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
+        kw = {}
+        if epi == ops.EPI_RESID:
+            res = torch.randn(L, N, device=dev, generator=g)
+            kw = dict(gate=torch.randn(N, device=dev, generator=g), res=res, aux=aux, out=res)
+        elif epi == ops.EPI_GELU:
+            kw = dict(aux=aux)
+        dy = (torch.randn(L, N, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        for i in range(reps):
+            for pas, fn in (("fwd", lambda: ops.linear_t(x, wt, bias, epi, **kw)),
+                            ("dx", lambda: ops.linear_dx(dy, w)), ("dw", lambda: ops.linear_dw(dy, x))):
+                torch.cuda.synchronize()
+                t0 = time.time()
+                fn()
+                torch.cuda.synchronize()
+                dt = time.time() - t0
+                print(f"gemm {pas} {name} {L}x{N}x{K} {dt*1e3:.2f} ms  {2*L*N*K/dt/1e12:.0f} TF/s",
+                      flush=True)
+        del x, w32, wt, w, aux, kw, dy
 elif which == "gemmcmp":
     # the QKV forward GEMM through prfl_gemm and through torch.matmul (hipBLASLt), same operands:
     # PMC comparison of MFMA busy, clock (GRBM_GUI_ACTIVE / 8 / wall) and instruction mix
