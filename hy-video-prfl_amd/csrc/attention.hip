@@ -119,8 +119,8 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
 // nbh % 8 != 0 keeps the plain order.  Measured at 720p x 81f (tools/ab_attn.py, one box, six
 // interleaved rounds, profiles/r02_ab_attn_xcd.txt): forward L2-miss traffic 30.4 -> 17.6 GB
 // per launch (FETCH_SIZE x 2), time 98.59 -> 98.34 ms (unchanged: the kernel is not memory
-// bound); the same grouping made dK/dV + dQ 2.3 % SLOWER, so the backward kernels keep the plain
-// (tile, head, sample) grid.
+// bound); in round 2 the same grouping made dK/dV + dQ 2.3 % SLOWER; round 5 re-measured it per
+// backward kernel (ATTN_BWD_XCD_* below): on for dQ, off for dK/dV.
 __device__ __forceinline__ void xcd_tile(int ntile, int nbh, int& bh, int& tile, int bid) {
   if ((nbh & 7) == 0) {
     const int i = bid >> 3, per = nbh >> 3;
@@ -147,11 +147,15 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
     t = unit % ntile;
   }
 }
+// Round 5, 720p x 81f, rocprofv3 --pmc of each kernel (profiles/r05_pmc_attn_bwd720_xcd.txt) and
+// one-process A/Bs (profiles/r05_ab_bwd_xcd.txt): the grouping takes the dQ kernel's fabric
+// traffic from 170 GB to 16.8 GB per launch at equal time (backward 311.11 vs 310.75 ms, 8 reps)
+// -- on; on the dK/dV kernel it RAISES it from 39 to 166 GB and costs 1.3 % -- off
 #ifndef ATTN_BWD_XCD_KV
 #define ATTN_BWD_XCD_KV 0
 #endif
 #ifndef ATTN_BWD_XCD_Q
-#define ATTN_BWD_XCD_Q 0
+#define ATTN_BWD_XCD_Q 1
 #endif
 // dQ kernel K / V ring depth: 2 (tile t+1 issued during tile t) or 3 (tile t+2: 144 KiB of LDS)
 #ifndef ATTN_DQ_STAGES

@@ -689,9 +689,43 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
 __device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
+
+// A64: a K-major A operand staged 64 deep.  A 32-deep K-major slice moves each A row as a 64-B
+// run (one LDS-DMA piece = 16 rows x 64 B = 16 half cache lines); staged 64 deep, a piece is 8
+// rows x 128 B = 8 whole lines, as hipBLASLt's MT256x256x64 TN loop fetches its operands.  The A
+// operand gets its own ring of three 64-deep slots (3 x 32 KiB) beside the B operand's ring of
+// four 32-deep slots (4 x 16 KiB): exactly the 160 KiB of LDS.  The 32-deep step schedule is
+// unchanged (one barrier per 32-deep sub-slice, fragments of sub-slice j+1 read during the MFMAs
+// of sub-slice j, 8 DMA pieces per wave per step, vmcnt(8)); A slice J (sub-slices 2J, 2J+1) is
+// issued half per step in steps 2J-4 and 2J-3 into slot J % 3, whose previous slice J-3 was last
+// read in step 2J-6, and it is retired by the vmcnt(8) + barrier at the top of step 2J-1, the
+// first that reads it.  Same MFMAs in the same k order: outputs bit-identical.
+// A 64-deep slot image: row r (0..255) at r * 128 B, 16-B chunk c (k 8c..8c+7) at c ^ (r & 7)
+// (the 128 kernel's conflict-free K-major layout).
+#ifndef GEMM4_A64
+#define GEMM4_A64 1
+#endif
+constexpr int A64SLOT = 32768;
+
+// byte offset of this lane's 16 B in A piece i (< 4) of half 0 of the wave's 64 rows of a 64-deep
+// slice at k0 = 0 (half 1 = rows + 32: the same lane offsets plus a wave-uniform soffset)
+__device__ __forceinline__ uint32_t piece_off_a64(int64_t ld, int wid, int lane, int i) {
+  const int row = (wid * 8 + i) * 8 + (lane >> 3), p = lane & 7;
+  return (uint32_t)(row * ld * 2) + ((p ^ (row & 7)) << 4);
+}
+
+// 16x16x32 A fragment of half h (k 32h..32h+31) of a 64-deep slot: lane l gets row
+// base + (l & 15), k = 32h + 8 (l >> 4) + 0..7
+__device__ __forceinline__ bf16x8 read_frag_a64(const char* slot, int h, int base, int lane) {
+  const int row = base + (lane & 15), kc = 4 * h + (lane >> 4);
+  return *(const bf16x8*)(slot + row * 128 + ((kc ^ (row & 7)) << 4));
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
+  constexpr bool A64 = A_KC && GEMM4_A64;
+  __shared__ __attribute__((aligned(16))) char smem[A64 ? 3 * A64SLOT + 4 * HALF4 : 4 * SLICE4];
+  char* const smB = smem + 3 * A64SLOT;      // A64: the B ring (4 x 16 KiB) after the A ring
   int tm, tn;
   tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
   const int m0 = tm * BM2, n0 = tn * BN2;
@@ -724,13 +758,25 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   uint32_t offa[4], offb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    offa[i] = piece_off4<A_KC>(g.lda, wid, lane, i) - i * 1024;
+    offa[i] = (A64 ? piece_off_a64(g.lda, wid, lane, i) : piece_off4<A_KC>(g.lda, wid, lane, i)) - i * 1024;
     offb[i] = piece_off4<B_KC>(g.ldb, wid, lane, i) - i * 1024;
   }
   unsigned m0keep = 0;
   // k0 -> soffset: 2 B per k for K-major operands, one row (ld elements) per k for MN-major
   auto soff_a = [&](int j) { return (uint32_t)(A_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.lda * 2); };
   auto soff_b = [&](int j) { return (uint32_t)(B_KC ? j * BK4 * 2 : (int64_t)j * BK4 * g.ldb * 2); };
+  // A64: piece i (< 4) of half hh of 64-deep A slice J into the A slot at sa; B piece i (< 4) of
+  // 32-deep sub-slice j into the B slot at sb
+  auto piece_a64 = [&](int i, int J, int hh, char* sa) {
+    if (i == 0) m0_set(lds_addr(sa + wid * 8192 + hh * 4096), m0keep);
+    dma16_buf_m0(srd_a, offa[i], (uint32_t)(J * 128 + (int64_t)hh * 32 * g.lda * 2), i);
+    if (i == 3) m0_restore(m0keep);
+  };
+  auto piece_b = [&](int i, int j, char* sb) {
+    if (i == 0) m0_set(lds_addr(sb + wid * 4096), m0keep);
+    dma16_buf_m0(srd_b, offb[i], soff_b(j), i);
+    if (i == 3) m0_restore(m0keep);
+  };
   // piece i (< 8: A pieces 0-3, B pieces 4-7) of slice j into ring slot sd
   auto piece = [&](int i, int j, char* sd) {
     if (i == 0 || i == 4) m0_set(lds_addr(sd + (i ? HALF4 : 0) + wid * 4096), m0keep);
@@ -809,14 +855,82 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
     }
   };
 
+  // A64 step j: MFMAs of sub-slice j || reads of sub-slice j+1 (A: half hr of the slot at ra; B:
+  // slot (j+1) & 3) || DMA of half hh of A slice J into the slot at sa and of B sub-slice j+3
+  auto step64 = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8],
+                    char* sa, int J, int hh, const char* ra, int hr) {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own pieces of sub-slice j+1 landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int jb = min(j + 3, ns - 1);
+    char* sb = smB + ((j + 3) & 3) * HALF4;
+    const char* rb = smB + ((j + 1) & 3) * HALF4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      mfma16(acc[i][0], cb[0], ca[i]);
+      if (i < 4) piece_a64(i, J, hh, sa);
+      else piece_b(i - 4, jb, sb);
+      mfma16(acc[i][1], cb[1], ca[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      na[i] = read_frag_a64(ra, hr, wm * 128 + i * 16, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma16(acc[i][2], cb[2], ca[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      nb[i] = read_frag4<B_KC>(rb, wn * 128 + i * 16, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jj = 3; jj < 8; ++jj) mfma16(acc[i][jj], cb[jj], ca[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   asm volatile("s_nop 7" ::: "memory");    // accumulator zeroing (VALU) -> first asm MFMA
+  bf16x8 fa[8], fb[8], ga[8], gb[8];
+  if constexpr (A64) {
+    // prologue: A slice 0, B 0, B 1, A slice 1, B 2; retire A 0 + B 0 (the last 16 pieces stay
+    // in flight) and read sub-slice 0
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) piece_a64(i, 0, hh, smem);
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) piece_b(i, jb, smB + jb * HALF4);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) piece_a64(i, 1, hh, smem + A64SLOT);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) piece_b(i, 2, smB + 2 * HALF4);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      fa[i] = read_frag_a64(smem, 0, wm * 128 + i * 16, lane);
+      fb[i] = read_frag4<B_KC>(smB, wn * 128 + i * 16, lane);
+    }
+    if (GEMM4_PREWAIT) __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    // A slots of A slices q, q+1, q+2 (q = j / 2), rotated every two steps
+    int s0 = 0, s1 = A64SLOT, s2 = 2 * A64SLOT;
+    const int nA = ns >> 1;
+    for (int j = 0; j < ns; j += 2) {
+      const int J = min((j >> 1) + 2, nA - 1);   // past the end: re-fetch the last slice
+      step64(j, fa, fb, ga, gb, smem + s2, J, 0, smem + s0, 1);
+      step64(j + 1, ga, gb, fa, fb, smem + s2, J, 1, smem + s1, 0);
+      const int t = s0;
+      s0 = s1;
+      s1 = s2;
+      s2 = t;
+    }
+  } else {
   issue(0);
   issue(1);
   issue(2);
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  bf16x8 fa[8], fb[8], ga[8], gb[8];
   read(0, fa, fb);
   // GEMM4_PREWAIT: retire every LDS / scalar load before the loop with a wait the compiler's
   // waitcnt pass sees (the builtin, not asm): else a kernel-argument load still in flight from
@@ -828,6 +942,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   for (int j = 0; j < ns; j += 2) {
     step(j, fa, fb, ga, gb);
     step(j + 1, ga, gb, fa, fb);
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // the MFMAs are inline asm: the compiler does not see their AGPR writes, so pad the

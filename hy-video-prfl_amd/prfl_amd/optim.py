@@ -46,7 +46,9 @@ class AdamW:
                 loads[r] += self.params[i].numel()
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.state = {}
-        self.step_count = 0
+        self.step_count = 0         # optimizer steps taken
+        self._pstep = {}            # per-parameter update count (torch's state['step']): the bias
+        #                             correction of a parameter that skipped a window lags behind
         self.state_on_host = state_on_host
         self.overlap = overlap
         self.ring_slots = ring_slots
@@ -141,6 +143,8 @@ class AdamW:
             self._zeroed.update(live)
         else:
             self._zeroed.difference_update(live)
+        for p in live:
+            self._pstep[p] = self._pstep.get(p, 0) + 1
         if not live:
             return
         if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
@@ -192,7 +196,7 @@ class AdamW:
             m, v = self._state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             ops.adamw_(p.data, g, m, v, lr, self.betas[0], self.betas[1], self.eps,
-                       self.weight_decay, self.step_count, zero_grad=zero_grad)
+                       self.weight_decay, self._pstep[p], zero_grad=zero_grad)
             if zero_grad and g is not p.grad:
                 p.grad.zero_()
             ev = torch.cuda.Event()
@@ -237,7 +241,7 @@ class AdamW:
             opt.wait_event(h2d_ev[i])
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             ops.adamw_(p.data, g, m_d[:n].view_as(p), v_d[:n].view_as(p), lr, self.betas[0],
-                       self.betas[1], self.eps, self.weight_decay, self.step_count,
+                       self.betas[1], self.eps, self.weight_decay, self._pstep[p],
                        zero_grad=zero_grad)
             if zero_grad and g is not p.grad:
                 p.grad.zero_()
@@ -258,7 +262,7 @@ class AdamW:
         for p in mine:
             m, v = self._state(p)
             ops.adamw_(p.data, p.grad, m, v, lr, self.betas[0], self.betas[1], self.eps,
-                       self.weight_decay, self.step_count)
+                       self.weight_decay, self._pstep[p])
         if self.shard:
             import torch.distributed as dist
             for p in live:
@@ -278,7 +282,8 @@ class AdamW:
         self.synchronize()
         idx = {id(p): i for i, p in enumerate(self.params)}
         return {"step": self.step_count,
-                "state": {idx[id(p)]: {"exp_avg": m.view_as(p), "exp_avg_sq": v.view_as(p)}
+                "state": {idx[id(p)]: {"step": self._pstep.get(p, 0), "exp_avg": m.view_as(p),
+                                       "exp_avg_sq": v.view_as(p)}
                           for p, (m, v) in self.state.items()}}
 
 
