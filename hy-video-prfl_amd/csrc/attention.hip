@@ -171,6 +171,34 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
 #ifndef ATTN_DQ_STAGGER
 #define ATTN_DQ_STAGGER 0
 #endif
+// dQ kernel, software-pipelined within the wave (round 5): per key sub-tile kt the work is
+// G1(kt) (S and dP, 16 MFMAs) -> V(kt) (exp, dS, bf16 pack: VALU only, depends on G1(kt)) ->
+// G2(kt) (dQ += K^T dS, 8 MFMAs, depends on V(kt)).  Written in that order, the two waves of a
+// SIMD reach V together (lockstep, one barrier per tile) and the matrix pipe idles through both
+// softmax blocks (PMC: MFMA busy 0.65, SQ_WAIT_INST 27 %).  PIPE issues each sub-tile's V beside
+// the previous sub-tile's G2 MFMAs: G1(0) V(0) G1(1) [V(1) || G2(0)] G1(2) [V(2) || G2(1)] G2(2),
+// the pairs interleaved by sched_group_barrier (2 LDS reads, 1 MFMA, 6 VALU per step); the tail
+// mask is a tile-level branch outside the interleaved regions.  Registers: one more packed dS
+// (8 VGPRs).  Same operations per element in the same order: outputs bit-identical.
+#ifndef ATTN_DQ_IL
+#define ATTN_DQ_IL 1
+#endif
+#ifndef ATTN_DQ_PIPE
+#define ATTN_DQ_PIPE 0
+#endif
+
+// one interleaved scheduling region: N x {D LDS reads, 1 MFMA, V VALU} (sched_group_barrier
+// masks: 0x100 DS read, 0x008 MFMA, 0x002 VALU | 0x400 TRANS)
+template <int N, int D, int V>
+__device__ __forceinline__ void sgb_interleave() {
+  if (!ATTN_DQ_IL) return;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x402, V, 0);   // VALU incl. transcendentals
+  }
+}
 
 __device__ __forceinline__ float xhalf_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -862,7 +890,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int TK = NKT * 32, SV = NKT * 8192, SB = (KT ? 3 : 2) * SV;
   constexpr int NST = KT ? 2 : ATTN_DQ_STAGES;               // ring stages of [K (image B) | V (| K^T)]
   static_assert(!KT || (NKT == 3 && !ATTN_DQ_STAGGER), "KT: 2 stages of 96-key tiles");
-  __shared__ __attribute__((aligned(16))) char smem[NST * SB];
+  constexpr bool PIPE = ATTN_DQ_PIPE && !KT && NST == 2 && !ATTN_DQ_STAGGER && NKT == 3;
+  // PIPE: the workgroup's 256 dO rows staged once after the K / V ring (64 KiB: 160 KiB total)
+  __shared__ __attribute__((aligned(16))) char smem[NST * SB + (PIPE ? 65536 : 0)];
   int unit, share;
   bool part;
   tail_unit(a.nmain_q, a.split_q, unit, share, part);
@@ -885,7 +915,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
     qf[ks] = *(const bf16x8*)(Qb + (int64_t)qr * a.ldq + ks * 16 + hh * 8);
-    df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
+    if (!PIPE) df[ks] = *(const bf16x8*)(dOb + (int64_t)qr * a.lddo + ks * 16 + hh * 8);
+  }
+  char* const dOs = smem + NST * SB;
+  if (PIPE) {   // dO rows q0 .. q0+255 (off16 image, row reads): 64 pieces of 4 rows, 8 per wave
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = w * 8 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
+      const int qrow = min(q0 + row, a.Lq - 1);
+      dma16(dOb + (int64_t)qrow * a.lddo + ((pc ^ (row & 15)) << 3), lds_addr(dOs + piece * 1024));
+    }
   }
   const float lse = a.LSE[((int64_t)b * a.H + h) * a.Lq + qr];
   const float del = a.Delta[((int64_t)b * a.H + h) * a.Lq + qr];
@@ -894,7 +933,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // score; the tuple costs 16 VGPRs, paid for by packing dS one key sub-tile at a time
   f32x16 lset;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lset[r] = ATTN_DQ_STAGES == 3 ? 0.f : lse;
+  for (int r = 0; r < 16; ++r) lset[r] = (ATTN_DQ_STAGES == 3 || PIPE) ? 0.f : lse;
   if (QS) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = -qf[ks];
@@ -974,6 +1013,77 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     if (!ATTN_BWD_DMA_MID && tn < nkv) dma(tn, stn);
     const char* Ks = smem + (NST == 3 ? t % 3 : (t & 1)) * SB;
     const char* Vs = Ks + SV;
+    if constexpr (PIPE) {
+      // G1(kt): S^T (started at this query's LSE under QS: 16 v_mov) and dP^T of key sub-tile kt,
+      // dO from its LDS image
+      auto g1 = [&](int kt, f32x16& st, f32x16& dpt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (QS) asm volatile("v_mov_b32 %0, %1" : "=v"(st[r]) : "v"(lse));
+          else st[r] = 0.f;
+          dpt[r] = 0.f;
+        }
+        const int row = kt * 32 + l32, qrow = w * 32 + l32;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
+          dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)),
+                       *(const bf16x8*)(dOs + off16(qrow, ks * 2 + hh)), dpt);
+        }
+      };
+      // V(kt): P and dS = P (dP - D) (D negated under NEGD); keys >= k_len masked (a uniform branch,
+      // taken in the tile holding k_len only); packed to bf16
+      auto val = [&](int kt, const f32x16& st, f32x16& dpt, bf16x8 (&dsp)[2]) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = QS ? __builtin_amdgcn_exp2f(-st[r]) : __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
+          dpt[r] = ATTN_BWD_NEGD ? p * (dpt[r] + del) : p * (dpt[r] - del);
+        }
+        if (__builtin_expect(kb + kt * 32 + 32 > a.k_len, 0)) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) dpt[r] = 0.f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          dsp[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
+                             f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
+                             f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+      };
+      // G2(kt): dQ^T += K^T dS^T (per dQ tile the same (kt, s2) summation order)
+      auto g2 = [&](int kt, const bf16x8 (&dsp)[2]) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int ra = kt * 32 + 16 * s2 + 4 * (g >> 1) + qq;
+            const bf16x8 kf = cat8(lds_read_tr(Ks + offB(ra, byte)), lds_read_tr(Ks + offB(ra + 8, byte)));
+            dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
+          }
+        }
+      };
+      f32x16 sa, pa, sb, pb;
+      bf16x8 dA[2], dB[2];
+      g1(0, sa, pa);                                          // G1(0)
+      __builtin_amdgcn_sched_barrier(0);
+      g1(1, sb, pb);                                          // G1(1) || V(0)
+      val(0, sa, pa, dA);
+      sgb_interleave<16, 2, 3>();
+      __builtin_amdgcn_sched_barrier(0);
+      if (ATTN_BWD_DMA_MID && tn < nkv) dma(tn, stn);
+      __builtin_amdgcn_sched_barrier(0);
+      g1(2, sa, pa);                                          // G1(2) || G2(0) || V(1)
+      g2(0, dA);
+      val(1, sb, pb, dB);
+      sgb_interleave<24, 2, 2>();
+      __builtin_amdgcn_sched_barrier(0);
+      g2(1, dB);                                              // G2(1) || V(2)
+      val(2, sa, pa, dA);
+      sgb_interleave<8, 2, 5>();
+      __builtin_amdgcn_sched_barrier(0);
+      g2(2, dA);                                              // G2(2)
+    } else {
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       f32x16 st, dpt;
@@ -1022,6 +1132,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
           dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
         }
       }
+    }
     }
     if (!ATTN_DQ_STAGGER && NST == 3 && tn < nkv)   // tile t+1 landed; t+2 may stay in flight
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");

@@ -838,8 +838,8 @@ def test_adamw_zero_grad_skips_untouched_like_set_to_none(ops):
                                    c.parameters()):
         assert torch.equal(pa, pb), n
         assert rel(pa, pr) <= 1e-3, (n, rel(pa, pr))   # kernel vs torch rounding through 6 steps
-    assert not torch.equal(a.blocks[1].weight, c.blocks[1].weight)
-    assert torch.equal(a.blocks[0].weight, c.blocks[0].weight)
+    # round-4 semantics: the bypassed block decays in the windows it sat out (and the model drifts)
+    assert rel(c.blocks[1].weight, a.blocks[1].weight) > 1e-4
 
 
 def test_adamw_overlap_zero_grad_requires_attach(ops):
