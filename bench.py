@@ -170,6 +170,17 @@ def cpu_baseline():
                 nproc=os.cpu_count())
 
 
+def cores_per_socket():
+    """Physical cores of one socket ('cpu cores' in /proc/cpuinfo), or None."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("cpu cores"):
+                return int(line.split(":")[1])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_attn_fwd720_vt_final.txt")
 
 
@@ -521,6 +532,15 @@ def main():
                                         f"to one PRFL iteration ({flops_it / 1e15:.1f} PFLOP)"))}
         if not c1:
             res["cpu_baseline"]["derived"] = "extrapolated (no full iteration runs on the CPU)"
+        cps = cores_per_socket()
+        if cps and cps > cb["threads"]:
+            # the GPU box grants this process a 16-CPU share of the host: the full socket is not
+            # measurable here.  Upper bound = linear scaling from the measured threads to every
+            # physical core of one socket (profiles/r05_cpu_thread_scaling.txt: 8 -> 16 threads)
+            res["cpu_baseline"]["full_socket_bound"] = {
+                "value": res["cpu_baseline"]["value"] * cps / cb["threads"], "cores": cps,
+                "kind": "bound", "what": f"linear-scaling upper bound: {cb['threads']} measured "
+                                         f"threads -> {cps} physical cores of one socket"}
     res["wall_s_at_report"] = round(time.time() - T_START, 1)
     print(json.dumps(res), flush=True)
     if world > 1:

@@ -183,6 +183,11 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
 #ifndef ATTN_DQ_IL
 #define ATTN_DQ_IL 1
 #endif
+// dQ: the LSE start of the S^T chain rebuilt per sub-tile by 16 v_mov instead of a loop-invariant
+// 16-VGPR tuple (frees registers for LDS read-ahead; A/B in profiles/r05_ab_dq_variants.txt)
+#ifndef ATTN_DQ_MOVLSE
+#define ATTN_DQ_MOVLSE 0
+#endif
 #ifndef ATTN_DQ_PIPE
 #define ATTN_DQ_PIPE 0
 #endif
@@ -267,6 +272,12 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // P exceeded 2^TAU (S' recomputed from the still-staged K tile), instead of a max pass over every
 // tile: 720p forward 89.94 -> 88.28 ms, bit-identical while no rescale triggers
 // (profiles/r03_ab_attn_sumcheck.txt); 0 = max pass every tile
+// QS forward: the row sums of P accumulated in pairs (v_pk_add_f32: one VALU issue per two
+// scores instead of one per score; the pair is folded once per tile).  Changes the fp32 summation
+// order of l, not the algorithm
+#ifndef ATTN_PKSUM
+#define ATTN_PKSUM 1
+#endif
 #ifndef ATTN_SUMCHECK
 #define ATTN_SUMCHECK 1
 #endif
@@ -482,14 +493,28 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         max_first = __any(m == NEG_INF);
         if (!max_first) {
           float ts = 0.f;
+          if (ATTN_PKSUM) {
+            f32x2 t2 = {0.f, 0.f};
 #pragma unroll
-          for (int kt = 0; kt < NKT; ++kt)
+            for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float p = __builtin_amdgcn_exp2f(s[kt][r]);
-              s[kt][r] = p;
-              ts += p;
-            }
+              for (int r = 0; r < 16; r += 2) {
+                const f32x2 p = {__builtin_amdgcn_exp2f(s[kt][r]), __builtin_amdgcn_exp2f(s[kt][r + 1])};
+                s[kt][r] = p[0];
+                s[kt][r + 1] = p[1];
+                t2 += p;
+              }
+            ts = t2[0] + t2[1];
+          } else {
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kt][r]);
+                s[kt][r] = p;
+                ts += p;
+              }
+          }
           if (__any(!(ts <= (float)(1 << ATTN_LAZY_TAU)))) {
             const char* Ks = smem + st * SB;
 #pragma unroll
@@ -527,14 +552,28 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) s[kt][r] -= d;     // (rare: the row max grew)
         }
+        if (ATTN_PKSUM) {
+          f32x2 t2 = {0.f, 0.f};
 #pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
+          for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = __builtin_amdgcn_exp2f(s[kt][r]);
-            s[kt][r] = p;
-            lsum += p;
-          }
+            for (int r = 0; r < 16; r += 2) {
+              const f32x2 p = {__builtin_amdgcn_exp2f(s[kt][r]), __builtin_amdgcn_exp2f(s[kt][r + 1])};
+              s[kt][r] = p[0];
+              s[kt][r + 1] = p[1];
+              t2 += p;
+            }
+          lsum += t2[0] + t2[1];
+        } else {
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float p = __builtin_amdgcn_exp2f(s[kt][r]);
+              s[kt][r] = p;
+              lsum += p;
+            }
+        }
       }
       if (QS) {
 #pragma unroll
@@ -636,6 +675,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 // dV / dK d-tile (3 = both); 0 / 1 / 2 / 3 tie within 0.3 % (profiles/r04_ab_dkdv_sb.txt)
 #ifndef ATTN_DKDV_SB
 #define ATTN_DKDV_SB 3
+#endif
+// dK/dV tail rows (round 5): the query rows past Lq of the last tile get LSE = +inf in LDS once
+// per tail tile, instead of a masking branch per row group inside every slice (the four uniform
+// branches split the softmax block into four scheduling regions: the exp / dS VALU could not be
+// moved between MFMAs).  P = exp2(-inf) = 0 exactly and dS = 0 * finite = 0: bit-identical.
+#ifndef ATTN_DKDV_INFTAIL
+#define ATTN_DKDV_INFTAIL 1
 #endif
 // static priority 1 for waves 4-7 of the backward kernels (MI355X guide, two waves per SIMD,
 // item 4): bit 0 dK/dV, bit 1 dQ
@@ -769,6 +815,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     const float* Ls = (const float*)(Qs + 32768);
     const int qb = (t0 + t) * 64;
     const bool tail = qb + 64 > a.Lq;
+    if (ATTN_DKDV_INFTAIL && __builtin_expect(tail, 0)) {
+      // the tile holding Lq: its rows past Lq landed as zeros (Q, dO, LSE, D); give them LSE =
+      // +inf, so P = exp2(S' - LSE) = 0 and dS = P (dP - D) = 0 with no mask in the slice body
+      if (w == 0 && qb + lane >= a.Lq) ((float*)Ls)[lane] = __builtin_inff();
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 sacc, dpt;
@@ -811,7 +865,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
           sacc[rg * 4 + r] = p;
           dpt[rg * 4 + r] = ATTN_BWD_NEGD ? p * dpt[rg * 4 + r] : p * (dpt[rg * 4 + r] - d4[r]);
         }
-        if (__builtin_expect(tail, 0)) {   // rows past Lq: P = dS = 0 (last tile only)
+        if (!ATTN_DKDV_INFTAIL && __builtin_expect(tail, 0)) {   // rows past Lq: P = dS = 0
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (qb + q4 + r >= a.Lq) { sacc[rg * 4 + r] = 0.f; dpt[rg * 4 + r] = 0.f; }
@@ -933,7 +987,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // score; the tuple costs 16 VGPRs, paid for by packing dS one key sub-tile at a time
   f32x16 lset;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lset[r] = (ATTN_DQ_STAGES == 3 || PIPE) ? 0.f : lse;
+  for (int r = 0; r < 16; ++r) lset[r] = (ATTN_DQ_STAGES == 3 || PIPE || ATTN_DQ_MOVLSE) ? 0.f : lse;
   if (QS) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = -qf[ks];
@@ -1090,13 +1144,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
       const int row = kt * 32 + l32;
-      if (QS && ATTN_DQ_STAGES == 3) {   // the LSE start rebuilt per sub-tile (16 v_mov): the
+      if (QS && (ATTN_DQ_STAGES == 3 || ATTN_DQ_MOVLSE)) {   // the LSE start rebuilt per sub-tile (16 v_mov): the
 #pragma unroll                            // loop-invariant 16-VGPR tuple would push the 3-stage
         for (int r = 0; r < 16; ++r)      // ring's bookkeeping into scratch
           asm volatile("v_mov_b32 %0, %1" : "=v"(st[r]) : "v"(lse));
       }
       st = mfma32(*(const bf16x8*)(Ks + offB(row, hh * 16)), qf[0],
-                  QS ? (ATTN_DQ_STAGES == 3 ? st : lset) : st);
+                  QS ? ((ATTN_DQ_STAGES == 3 || ATTN_DQ_MOVLSE) ? st : lset) : st);
       dpt = mfma32(*(const bf16x8*)(Vs + off16(row, hh)), df[0], dpt);
 #pragma unroll
       for (int ks = 1; ks < 8; ++ks) {

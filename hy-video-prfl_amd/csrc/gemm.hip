@@ -721,11 +721,29 @@ __device__ __forceinline__ bf16x8 read_frag_a64(const char* slot, int h, int bas
   return *(const bf16x8*)(slot + row * 128 + ((kc ^ (row & 7)) << 4));
 }
 
+// Start stagger: all 256 first-wave workgroups start together, so every CU reaches its epilogue
+// (the residual / pre-activation reads and the output writes) at the same moment and the chip's
+// HBM serves 256 epilogues at once while every matrix pipe idles; the next wave inherits the same
+// phase.  With GEMM4_STAGGER = S > 0 the first-wave workgroup of slot s = (bid >> 3) & 31 on its
+// XCD first waits s/32 * S * K shader cycles (S ~ 54 cycles per K is one tile's main loop at
+// 1.3 PF), so the CUs' epilogues fall at spread-out times from then on.  Grids of >= 2 waves only.
+#ifndef GEMM4_STAGGER
+#define GEMM4_STAGGER 0
+#endif
+__device__ __forceinline__ void gemm_start_stagger(int K) {
+  if (GEMM4_STAGGER && blockIdx.x < 256 && gridDim.x >= 512) {
+    const uint64_t wait = (uint64_t)((blockIdx.x >> 3) & 31) * (uint64_t)K * GEMM4_STAGGER / 32;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   constexpr bool A64 = A_KC && GEMM4_A64;
   __shared__ __attribute__((aligned(16))) char smem[A64 ? 3 * A64SLOT + 4 * HALF4 : 4 * SLICE4];
   char* const smB = smem + 3 * A64SLOT;      // A64: the B ring (4 x 16 KiB) after the A ring
+  gemm_start_stagger(g.K);
   int tm, tn;
   tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
   const int m0 = tm * BM2, n0 = tn * BN2;
@@ -1095,6 +1113,7 @@ __device__ __forceinline__ void epilogue4x(const GemmArgs& g, const f32x16 (&acc
 template <bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm4x_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLICE4];
+  gemm_start_stagger(g.K);
   int tm, tn;
   tile_coords2(blockIdx.x, g.M, g.N, tm, tn);
   const int m0 = tm * BM2, n0 = tn * BN2;
