@@ -205,6 +205,18 @@ def big_fits(args):
     return args.workload.startswith("prfl") and args.workload.endswith("720")
 
 
+def host_moments(big):
+    """AdamW moments on the host: all of them at 720p (the memory plan); at 480p the
+    last fifth of the parameters in update order (the last 8 generator blocks: 23 GB of HBM back,
+    their ~0.8 s of PCIe per update hidden under the first 32 blocks' forwards).  PRFL_OPT_HOST
+    overrides: 1 = all, 0 = none, a fraction in (0, 1) = that tail."""
+    env = os.environ.get("PRFL_OPT_HOST")
+    if env is not None:
+        f = float(env)
+        return True if f >= 1.0 else (False if f <= 0.0 else f)
+    return True if big else 0.2
+
+
 def draw_mid(rank, world, dev):
     """mid_timestep = randint(0, 38) drawn on rank 0 and broadcast (train_prfl.py:640-651)."""
     t = torch.randint(0, 39, (1,), device=dev) if rank == 0 else torch.zeros(1, dtype=torch.long, device=dev)
@@ -343,7 +355,7 @@ def main():
             big = args.workload.endswith("720") or args.toy
             tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
                              feature_layer=(TOY_DIMS["lrm_layers"],) if args.toy else (8,),
-                             optimizer_state_on_host=big or os.environ.get("PRFL_OPT_HOST") == "1",
+                             optimizer_state_on_host=host_moments(big),
                              optimizer_shard=big and world > 1,
                              optimizer_overlap=os.environ.get("PRFL_OPT_OVERLAP", "1") == "1")
             if world > 1:

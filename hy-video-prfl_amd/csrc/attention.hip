@@ -179,17 +179,21 @@ __device__ __forceinline__ void bwd_unit(int unit, int ntile, int H, int B, int&
 // the previous sub-tile's G2 MFMAs: G1(0) V(0) G1(1) [V(1) || G2(0)] G1(2) [V(2) || G2(1)] G2(2),
 // the pairs interleaved by sched_group_barrier (2 LDS reads, 1 MFMA, 6 VALU per step); the tail
 // mask is a tile-level branch outside the interleaved regions.  Registers: one more packed dS
-// (8 VGPRs).  Same operations per element in the same order: outputs bit-identical.
+// (8 VGPRs) and dO staged in LDS; it spills 72 B and hipcc still keeps the exps in one block.
+// Same operations per element in the same order: outputs bit-identical, but the 720p backward
+// runs 309.26 -> 326.62 ms (one process, profiles/r05_ab_dq_variants.txt): off
+#ifndef ATTN_DQ_PIPE
+#define ATTN_DQ_PIPE 0
+#endif
+// (PIPE only) the interleave of each region by sched_group_barrier
 #ifndef ATTN_DQ_IL
 #define ATTN_DQ_IL 1
 #endif
 // dQ: the LSE start of the S^T chain rebuilt per sub-tile by 16 v_mov instead of a loop-invariant
-// 16-VGPR tuple (frees registers for LDS read-ahead; A/B in profiles/r05_ab_dq_variants.txt)
+// 16-VGPR tuple (240 VGPRs instead of 256, no spill): 1.3 % slower at 720p, 1.4 % at 480p
+// (profiles/r05_ab_dq_variants.txt): off
 #ifndef ATTN_DQ_MOVLSE
 #define ATTN_DQ_MOVLSE 0
-#endif
-#ifndef ATTN_DQ_PIPE
-#define ATTN_DQ_PIPE 0
 #endif
 
 // one interleaved scheduling region: N x {D LDS reads, 1 MFMA, V VALU} (sched_group_barrier
@@ -272,11 +276,12 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // P exceeded 2^TAU (S' recomputed from the still-staged K tile), instead of a max pass over every
 // tile: 720p forward 89.94 -> 88.28 ms, bit-identical while no rescale triggers
 // (profiles/r03_ab_attn_sumcheck.txt); 0 = max pass every tile
-// QS forward: the row sums of P accumulated in pairs (v_pk_add_f32: one VALU issue per two
-// scores instead of one per score; the pair is folded once per tile).  Changes the fp32 summation
-// order of l, not the algorithm
+// QS forward: the row sums of P accumulated in pairs (v_pk_add_f32: one VALU instruction per two
+// scores instead of one per score; the pair is folded once per tile).  Measured 11.7 % SLOWER at
+// 720p (85.14 -> 95.14 ms) and 10.1 % at 480p, same error vs fp64 (profiles/r05_ab_attn_pksum.txt):
+// packed f32 beside MFMAs costs far more than its issue slot (MI355X guide, constants table).  Off
 #ifndef ATTN_PKSUM
-#define ATTN_PKSUM 1
+#define ATTN_PKSUM 0
 #endif
 #ifndef ATTN_SUMCHECK
 #define ATTN_SUMCHECK 1
@@ -679,9 +684,11 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 // dK/dV tail rows (round 5): the query rows past Lq of the last tile get LSE = +inf in LDS once
 // per tail tile, instead of a masking branch per row group inside every slice (the four uniform
 // branches split the softmax block into four scheduling regions: the exp / dS VALU could not be
-// moved between MFMAs).  P = exp2(-inf) = 0 exactly and dS = 0 * finite = 0: bit-identical.
+// moved between MFMAs).  P = exp2(-inf) = 0 exactly and dS = 0 * finite = 0: bit-identical,
+// but the one-region body schedules WORSE: 720p backward 308.80 -> 315.44 ms, 480p 60.54 -> 61.88
+// (one process, profiles/r05_ab_dq_variants.txt), so it stays off
 #ifndef ATTN_DKDV_INFTAIL
-#define ATTN_DKDV_INFTAIL 1
+#define ATTN_DKDV_INFTAIL 0
 #endif
 // static priority 1 for waves 4-7 of the backward kernels (MI355X guide, two waves per SIMD,
 // item 4): bit 0 dK/dV, bit 1 dQ

@@ -558,20 +558,49 @@ __device__ __forceinline__ bf16x8 read_frag4(const char* lds, int base, int lane
 #ifndef EPI4_AHEAD
 #define EPI4_AHEAD 3
 #endif
+// EPI4_LDSCOEF: the bias / gate coefficients of the wave's 128 columns staged in LDS (free once the
+// main loop's DMA has landed) and read per fragment, instead of 64 VGPRs held through the epilogue:
+// those registers go to residual / pre-activation loads further ahead (EPI4_AHEAD)
+#ifndef EPI4_LDSCOEF
+#define EPI4_LDSCOEF 0
+#endif
 template <int EPI, bool IN_BF16>
-__device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)[8][8], int mb, int nb) {
+__device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)[8][8], int mb, int nb,
+                                           char* coef) {
   constexpr bool HAS_IN = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_DGELU;
+  constexpr bool HAS_BIAS = EPI != EPI_F32 && EPI != EPI_DGELU, HAS_GATE = EPI == EPI_RESID;
   using InT = typename std::conditional<IN_BF16, bf16x4, f32x4>::type;
   float bias[8][4], gate[8][4];
+  if (EPI4_LDSCOEF) {
+    // coef: this wave's 1 KiB (bias[128] | gate[128] floats, column c = nb0 + c); lane l writes
+    // columns 2l, 2l + 1.  LDS operations of one wave complete in order: no barrier needed
+    const int lane = threadIdx.x & 63, nb0 = nb - 4 * (lane >> 4);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int n = nb + 16 * j;
+    for (int h = 0; h < 2; ++h) {
+      const int n = nb0 + 2 * lane + h;
+      ((float*)coef)[2 * lane + h] = (HAS_BIAS && g.bias && n < g.N) ? bf2f(g.bias[n]) : 0.f;
+      ((float*)coef)[128 + 2 * lane + h] = (HAS_GATE && g.gate && n < g.N) ? g.gate[n] : 1.f;
+    }
+  } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      bias[j][r] = (EPI != EPI_F32 && EPI != EPI_DGELU && g.bias && n < g.N) ? bf2f(g.bias[n + r]) : 0.f;
-      gate[j][r] = (EPI == EPI_RESID && g.gate && n < g.N) ? g.gate[n + r] : 1.f;
+    for (int j = 0; j < 8; ++j) {
+      const int n = nb + 16 * j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bias[j][r] = (HAS_BIAS && g.bias && n < g.N) ? bf2f(g.bias[n + r]) : 0.f;
+        gate[j][r] = (HAS_GATE && g.gate && n < g.N) ? g.gate[n + r] : 1.f;
+      }
     }
   }
+  // the coefficients of fragment jj: registers, or one 16-B LDS read each
+  auto cb = [&](int jj) {
+    if (!EPI4_LDSCOEF) return (f32x4){bias[jj][0], bias[jj][1], bias[jj][2], bias[jj][3]};
+    return *(const f32x4*)(coef + 4 * (4 * ((threadIdx.x & 63) >> 4) + 16 * jj));
+  };
+  auto cg = [&](int jj) {
+    if (!EPI4_LDSCOEF) return (f32x4){gate[jj][0], gate[jj][1], gate[jj][2], gate[jj][3]};
+    return *(const f32x4*)(coef + 512 + 4 * (4 * ((threadIdx.x & 63) >> 4) + 16 * jj));
+  };
   const void* src = EPI == EPI_F32 ? (const void*)g.C : EPI == EPI_DGELU ? (const void*)g.aux : g.res;
   const int64_t lds_in = EPI == EPI_F32 ? g.ldc : EPI == EPI_DGELU ? g.ldaux : g.ldr;
   const bool any_in = HAS_IN && (EPI != EPI_F32 || g.accumulate);
@@ -639,8 +668,9 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
             for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
           } else {
             float y[4];
+            const f32x4 bj = cb(jj);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bias[jj][r]);
+            for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bj[r]);
             if (EPI == EPI_BF16) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(y[r]);
@@ -653,10 +683,10 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
             } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
 #pragma unroll
               for (int r = 0; r < 4; ++r) ox[h][r] = f2bf(y[r]);
-              const f32x4 res = widen(buf[i][jj]);
+              const f32x4 res = widen(buf[i][jj]), gj = cg(jj);
               f32x4 o;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gate[jj][r]);
+              for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gj[r]);
               if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
             }
           }
@@ -967,10 +997,14 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   const int mb = m0 + wm * 128 + (lane & 15), nb = n0 + wn * 128 + 4 * (lane >> 4);
+  if (EPI4_LDSCOEF) {        // every wave's DMA has landed before any wave writes its LDS block
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
   if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
-    epilogue4w<EPI, true>(g, acc, mb, nb);
+    epilogue4w<EPI, true>(g, acc, mb, nb, smem + wid * 1024);
   else
-    epilogue4w<EPI, false>(g, acc, mb, nb);
+    epilogue4w<EPI, false>(g, acc, mb, nb, smem + wid * 1024);
 }
 
 // ---------------------------------------- 256x256, four waves, MFMA 32x32x16 (gemm4x) -------

@@ -8,6 +8,11 @@
                       fits 720p x 81f on one 288 GB GPU.  Both directions share ONE
                       copy stream: the host link moves 57 GB/s one way at a time but only
                       ~37 GB/s in total when H2D and D2H run concurrently (profiles/r01_pcie.txt).
+                      A fraction f in (0, 1) streams only the moments of the LAST tensors in
+                      update order (attach(): the last blocks a forward reads) covering f of the
+                      parameters and keeps the rest in HBM: the 480p plan (C3), where the whole
+                      stream (~4 s of PCIe per update) does not hide under a 480p rollout but a
+                      fifth of it does, and frees 23 GB of HBM.
     ``overlap``       the update runs on a side stream and step() returns without making the
                       caller's stream wait.  Every parameter gets a ready event; ``attach(model)``
                       installs forward pre-hooks so the first forward that reads a parameter
@@ -71,10 +76,31 @@ class AdamW:
     def _touch(self, p):
         self._touched.add(p)
 
+    def _host_params(self):
+        """The tensors whose moments live on the host: all (state_on_host True), none (False),
+        or the shortest tail of self.params (update order) holding >= f of the parameters."""
+        hp = getattr(self, "_host_set", None)
+        if hp is None:
+            f = self.state_on_host
+            if f is True or f is False:
+                hp = set(self.params) if f else set()
+            else:
+                f = float(f)
+                if not 0.0 < f <= 1.0:
+                    raise ValueError(f"state_on_host fraction must be in (0, 1], got {f}")
+                need, hp = f * sum(p.numel() for p in self.params), set()
+                for p in reversed(self.params):
+                    if need <= 0:
+                        break
+                    hp.add(p)
+                    need -= p.numel()
+            self._host_set = hp
+        return hp
+
     def _state(self, p):
         st = self.state.get(p)
         if st is None:
-            if self.state_on_host:
+            if p in self._host_params():
                 st = (torch.zeros(p.numel(), dtype=torch.float32, pin_memory=True),
                       torch.zeros(p.numel(), dtype=torch.float32, pin_memory=True))
             else:
@@ -120,6 +146,10 @@ class AdamW:
         rest = [p for p in model.parameters() if id(p) not in inner]
         order = {id(p): i for i, p in enumerate(rest + [p for g in groups for p in g.parameters()])}
         self.params.sort(key=lambda p: order.get(id(p), len(order)))
+        if self.state and getattr(self, "_host_set", None) is not None:
+            raise RuntimeError("attach() must precede the first step / init_state(): the host-"
+                               "moment tail is chosen in update order")
+        self._host_set = None
         self._hooks.append(model.register_forward_pre_hook(lambda m, a: self.wait(rest)))
         for g in groups:
             ps = list(g.parameters())
@@ -170,10 +200,12 @@ class AdamW:
                 for p in live:
                     if self.owner[p] != self.rank:
                         p.grad.zero_()
-            if self.state_on_host:
-                done = self._update_streamed(mine, lr, opt, cp, zero_grad)
-            else:
-                done = self._update_device(mine, lr, zero_grad)
+            host = self._host_params()
+            # device-resident moments first (the earlier tensors in update order), then the
+            # streamed tail: its first H2D copies start on `cp` at once, beside the device updates
+            done = self._update_device([p for p in mine if p not in host], lr, zero_grad)
+            done.update(self._update_streamed([p for p in mine if p in host], lr, opt, cp,
+                                              zero_grad))
             if self.shard:
                 import torch.distributed as dist
                 for p in live:

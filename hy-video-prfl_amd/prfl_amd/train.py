@@ -100,11 +100,11 @@ class PRFLTrainer:
         self.optimizer = AdamW(params, lr=lr, weight_decay=weight_decay,
                                state_on_host=optimizer_state_on_host, shard=optimizer_shard,
                                overlap=optimizer_overlap)
-        self.optimizer.init_state()
         if optimizer_overlap:
             # each block's forward waits for its own parameters' update (optim.py): the SFT
             # step's optimizer update streams under the reward step's rollout
             self.optimizer.attach(transformer)
+        self.optimizer.init_state()          # after attach: a host-moment fraction is a tail in update order
         self.reducer = GradReducer(params)
         self.grad_accum = grad_accum
         self.inference_steps = inference_steps

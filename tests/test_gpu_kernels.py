@@ -694,7 +694,7 @@ def test_adamw_overlapped_update_is_bit_exact(ops):
     torch.manual_seed(0)
     ref = Toy().to(DEV)
     x = torch.randn(32, 16, device=DEV)
-    for host in (False, True):
+    for host in (False, True, 0.4):      # 0.4: the streamed tail (last blocks + head), rest in HBM
         a, b = Toy().to(DEV), Toy().to(DEV)
         a.load_state_dict(ref.state_dict())
         b.load_state_dict(ref.state_dict())
@@ -702,6 +702,9 @@ def test_adamw_overlapped_update_is_bit_exact(ops):
         ob = AdamW(list(b.parameters()), lr=1e-2, state_on_host=host, overlap=True, ring_slots=2)
         ob.attach(b)
         assert ob.params[0] is b.emb.weight and ob.params[-1] is b.head.bias
+        if host == 0.4:
+            hp = ob._host_params()
+            assert b.head.bias in hp and b.emb.weight not in hp and 0 < len(hp) < len(ob.params)
         for it in range(4):
             la, lb = a(x).square().mean(), b(x).square().mean()   # b's forward waits per block
             assert torch.equal(la, lb), (host, it)

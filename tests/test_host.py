@@ -153,6 +153,34 @@ def test_train_model_and_save_model(tmp_path):
         train_model(MLP(8), "cpu", "clf", X, y, X, y, epochs=1)
 
 
+def test_adamw_host_moment_fraction_is_the_update_order_tail():
+    """state_on_host = f: the moments of the shortest tail of the parameters in update order
+    (attach(): embeddings, blocks 0..n-1, head) holding >= f of the elements live on the host."""
+    from prfl_amd.optim import AdamW
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = torch.nn.Linear(8, 32)
+            self.blocks = torch.nn.ModuleList([torch.nn.Linear(32, 32) for _ in range(10)])
+            self.head = torch.nn.Linear(32, 4)
+
+    m = Toy()
+    total = sum(p.numel() for p in m.parameters())
+    for f in (0.2, 0.5, 1.0):
+        opt = AdamW(list(m.parameters()), state_on_host=f)
+        opt.attach(m)
+        hp = opt._host_params()
+        n = sum(p.numel() for p in hp)
+        k = len(hp)
+        assert all(p in hp for p in opt.params[-k:]) and not any(p in hp for p in opt.params[:-k])
+        assert n >= f * total and n - opt.params[-k].numel() < f * total
+        assert m.head.weight in hp
+    assert AdamW(list(m.parameters()), state_on_host=False)._host_params() == set()
+    with pytest.raises(ValueError):
+        AdamW(list(m.parameters()), state_on_host=1.5)._host_params()
+
+
 def test_fp8_path_keeps_fp32_masters():
     """C5 quantises its e4m3 weights from the fp32 masters every pass: a bf16-stored trunk is
     refused in either order, and the PRFL trainer keeps an fp8 trunk in fp32."""
