@@ -170,6 +170,9 @@ def cpu_baseline():
                 nproc=os.cpu_count())
 
 
+CPU_SCALING_PER_DOUBLING = 1.33    # profiles/r05_cpu_thread_scaling.txt: 47.9 s -> 35.9 s
+
+
 def cores_per_socket():
     """Physical cores of one socket ('cpu cores' in /proc/cpuinfo), or None."""
     try:
@@ -549,10 +552,14 @@ def main():
             # the GPU box grants this process a 16-CPU share of the host: the full socket is not
             # measurable here.  Upper bound = linear scaling from the measured threads to every
             # physical core of one socket (profiles/r05_cpu_thread_scaling.txt: 8 -> 16 threads)
+            doublings = math.log2(cps / cb["threads"])
             res["cpu_baseline"]["full_socket_bound"] = {
                 "value": res["cpu_baseline"]["value"] * cps / cb["threads"], "cores": cps,
                 "kind": "bound", "what": f"linear-scaling upper bound: {cb['threads']} measured "
-                                         f"threads -> {cps} physical cores of one socket"}
+                                         f"threads -> {cps} physical cores of one socket",
+                "estimate_at_measured_scaling": res["cpu_baseline"]["value"] * CPU_SCALING_PER_DOUBLING ** doublings,
+                "scaling_source": f"{CPU_SCALING_PER_DOUBLING}x per thread doubling, 8 -> 16 threads on "
+                                  f"this workload (profiles/r05_cpu_thread_scaling.txt)"}
     res["wall_s_at_report"] = round(time.time() - T_START, 1)
     print(json.dumps(res), flush=True)
     if world > 1:

@@ -556,30 +556,70 @@ __device__ __forceinline__ bf16x8 read_frag4(const char* lds, int base, int lane
 // (res == C) stays correct: a row block is read before anything of it is written.  Same
 // arithmetic, in the same order, as epilogue_tile (outputs bit-identical to the 128 kernel).
 #ifndef EPI4_AHEAD
-#define EPI4_AHEAD 3
+#define EPI4_AHEAD 2
 #endif
-// EPI4_LDSCOEF: the bias / gate coefficients of the wave's 128 columns staged in LDS (free once the
-// main loop's DMA has landed) and read per fragment, instead of 64 VGPRs held through the epilogue:
-// those registers go to residual / pre-activation loads further ahead (EPI4_AHEAD)
-#ifndef EPI4_LDSCOEF
-#define EPI4_LDSCOEF 0
+// FULL (round 5): a tile whose 256 x 256 outputs are all in range, with 16-B aligned output rows
+// and 8 / 16-B aligned bias / gate (every tile of the 720p / 480p shapes), takes an epilogue with
+// no per-lane bounds test.  With the tests, every coefficient, residual and store sat in its own
+// exec-masked block (s_cbranch_execz per fragment): the waitcnt pass could not count across them
+// and drained vmcnt(0) at the joins, and each bias load (bf16, converted at once) was waited alone.
+// FULL: one batch of coefficient loads, counted waits; GELU / dGELU / biased forward 1-4 % faster
+// on the 720p shapes, the gated residual 0-2 % (profiles/r05_ab_gemm_full.txt).  Same arithmetic
+// in the same order: bit-identical.
+//
+// Measured and dropped: the whole residual tile issued before the first store (row blocks 0-4 by
+// LDS-DMA into the ring's 160 KiB, 5-7 into registers, one vmcnt(0), then no memory wait at all,
+// since vmcnt also counts stores): bit-identical and no faster than FULL alone
+// (profiles/r05_ab_gemm_stage.txt), so the residual's latency is not what the epilogue waits on.
+//
+// SH (EPI4_SHUFFLE, FULL tiles): the outputs leave through LDS.  In the MFMA layout a lane holds 4
+// columns of one row, so every store instruction wrote 16 rows x 64 B: 16 half cache lines per
+// instruction, and the per-CU store stream (not the residual loads, not the bandwidth) set the
+// epilogue's time -- fp32 C alone cost 14 us per tile more than bf16 C, at 32 tiles as at 5 760
+// (profiles/r05_gemm_epi_probe.txt).  SH writes each pass of 32 rows (two row blocks) of the
+// wave's 128 columns into a wave-private LDS image (rows padded 16 B: conflict-free both ways) and
+// reads it back row-major, so a store instruction writes 2 rows x 512 B (fp32) or 4 rows x 256 B
+// (bf16): whole lines.  Per wave 25 KiB: [32 rows x 528 B] fp32 / bf16 C | [32 x 272 B] bf16 aux.
+// Same values: bit-identical.
+#ifndef EPI4_SHUFFLE
+#define EPI4_SHUFFLE 1
 #endif
-template <int EPI, bool IN_BF16>
+constexpr int EPI4_WLDS = 32 * 528 + 32 * 272;    // 25 600 B of LDS per wave
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+template <int EPI, bool IN_BF16, bool FULL, bool SH = false>
 __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)[8][8], int mb, int nb,
-                                           char* coef) {
+                                           char* wl = nullptr) {
+  static_assert(!SH || FULL, "the LDS shuffle serves whole tiles only");
+  constexpr int AHEAD = EPI4_AHEAD;
+  constexpr bool F32C = EPI == EPI_F32 || EPI == EPI_RESID;          // C is fp32
+  constexpr bool HAS_AUX = EPI == EPI_GELU || EPI == EPI_RESID;
+  constexpr int RSF = 528, RSB = 272, AUX0 = 32 * 528;              // SH image strides / aux offset
   constexpr bool HAS_IN = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_DGELU;
   constexpr bool HAS_BIAS = EPI != EPI_F32 && EPI != EPI_DGELU, HAS_GATE = EPI == EPI_RESID;
   using InT = typename std::conditional<IN_BF16, bf16x4, f32x4>::type;
-  float bias[8][4], gate[8][4];
-  if (EPI4_LDSCOEF) {
-    // coef: this wave's 1 KiB (bias[128] | gate[128] floats, column c = nb0 + c); lane l writes
-    // columns 2l, 2l + 1.  LDS operations of one wave complete in order: no barrier needed
-    const int lane = threadIdx.x & 63, nb0 = nb - 4 * (lane >> 4);
+  // FULL: the bias kept as loaded (bf16, widened at use, so the batch of loads is not drained
+  // one by one by its conversion)
+  f32x4 bias[8], gate[8];
+  bf16x4 braw[8];
+  const bool fbias = FULL && HAS_BIAS && g.bias;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int n = nb0 + 2 * lane + h;
-      ((float*)coef)[2 * lane + h] = (HAS_BIAS && g.bias && n < g.N) ? bf2f(g.bias[n]) : 0.f;
-      ((float*)coef)[128 + 2 * lane + h] = (HAS_GATE && g.gate && n < g.N) ? g.gate[n] : 1.f;
+  for (int j = 0; j < 8; ++j) {
+    bias[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    gate[j] = (f32x4){1.f, 1.f, 1.f, 1.f};
+    braw[j] = bf16x4{};
+  }
+  if (FULL) {                    // uniform tests only: one batch of vector loads
+    if (fbias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) braw[j] = *(const bf16x4*)(g.bias + nb + 16 * j);
+    }
+    if (HAS_GATE && g.gate) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gate[j] = *(const f32x4*)(g.gate + nb + 16 * j);
     }
   } else {
 #pragma unroll
@@ -592,15 +632,6 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
       }
     }
   }
-  // the coefficients of fragment jj: registers, or one 16-B LDS read each
-  auto cb = [&](int jj) {
-    if (!EPI4_LDSCOEF) return (f32x4){bias[jj][0], bias[jj][1], bias[jj][2], bias[jj][3]};
-    return *(const f32x4*)(coef + 4 * (4 * ((threadIdx.x & 63) >> 4) + 16 * jj));
-  };
-  auto cg = [&](int jj) {
-    if (!EPI4_LDSCOEF) return (f32x4){gate[jj][0], gate[jj][1], gate[jj][2], gate[jj][3]};
-    return *(const f32x4*)(coef + 512 + 4 * (4 * ((threadIdx.x & 63) >> 4) + 16 * jj));
-  };
   const void* src = EPI == EPI_F32 ? (const void*)g.C : EPI == EPI_DGELU ? (const void*)g.aux : g.res;
   const int64_t lds_in = EPI == EPI_F32 ? g.ldc : EPI == EPI_DGELU ? g.ldaux : g.ldr;
   const bool any_in = HAS_IN && (EPI != EPI_F32 || g.accumulate);
@@ -610,7 +641,7 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
     for (int j = 0; j < 8; ++j) {
       const int n = nb + 16 * j;
       in[j] = InT{};
-      if (!any_in || m >= g.M || n >= g.N) continue;
+      if (!any_in || (!FULL && (m >= g.M || n >= g.N))) continue;
       in[j] = *(const InT*)((const char*)src + ((int64_t)m * lds_in + n) * sizeof(in[j][0]));
     }
   };
@@ -621,20 +652,21 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
     return f;
   };
   InT buf[8][8];
+  const int lane = threadIdx.x & 63;
   if (HAS_IN) {
 #pragma unroll
-    for (int i = 0; i < EPI4_AHEAD; ++i) load_in(i, buf[i]);
+    for (int i = 0; i < AHEAD; ++i) load_in(i, buf[i]);
   }
   // bf16 outputs of fragments j, j+1 leave as ONE 16-B store per lane (MI355X guide T21, with
   // v_permlane16_swap: lane group g holds columns 4g..4g+3 of a 16-column fragment; swapping
   // groups 1 <-> 0 and 3 <-> 2 between the two fragments gives every lane 8 contiguous columns,
   // at column offset 16 (g & 1) + 8 (g >> 1) of the pair) when the wave's 128 columns are in
   // range and the rows 16-B aligned; else the two 8-B stores as computed
-  const int gq = (threadIdx.x & 63) >> 4, nw = nb - 4 * gq;
+  const int gq = lane >> 4, nw = nb - 4 * gq;
   const int woff = 16 * (gq & 1) + 8 * (gq >> 1);
   const bool cols_in = nw + 128 <= g.N;
-  const bool wide_c = cols_in && (g.ldc % 8) == 0 && (((uintptr_t)g.C) & 15) == 0;
-  const bool wide_x = cols_in && (g.ldaux % 8) == 0 && (((uintptr_t)g.aux) & 15) == 0;
+  const bool wide_c = FULL || (cols_in && (g.ldc % 8) == 0 && (((uintptr_t)g.C) & 15) == 0);
+  const bool wide_x = FULL || (cols_in && (g.ldaux % 8) == 0 && (((uintptr_t)g.aux) & 15) == 0);
   auto st_pair = [&](bf16* base, int64_t ld, bool wide, int m, int j, bf16x4 a, bf16x4 b) {
     bf16* row = base + (int64_t)m * ld;
     if (wide) {
@@ -649,9 +681,9 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
   };
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    if (HAS_IN && i + EPI4_AHEAD < 8) load_in(i + EPI4_AHEAD, buf[i + EPI4_AHEAD]);
+    if (HAS_IN && i + AHEAD < 8) load_in(i + AHEAD, buf[i + AHEAD]);
     const int m = mb + 16 * i;
-    if (m < g.M) {
+    if (FULL || m < g.M) {
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         bf16x4 oc[2], ox[2];          // bf16 results for C / aux of fragments j, j + 1
@@ -660,17 +692,17 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
           const int jj = j + h, n = nb + 16 * jj;
           const f32x4 v = acc[i][jj];
           if (EPI == EPI_F32) {
-            if (n < g.N)
-              *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = g.accumulate ? v + widen(buf[i][jj]) : v;
+            const f32x4 o = g.accumulate ? v + widen(buf[i][jj]) : v;
+            if (SH) *(f32x4*)(wl + ((i & 1) * 16 + (lane & 15)) * RSF + (16 * jj + 4 * gq) * 4) = o;
+            else if (FULL || n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
           } else if (EPI == EPI_DGELU) {
             const f32x4 pre = widen(buf[i][jj]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(bfr(v[r]) * gelu_tanh_grad(pre[r]));
           } else {
             float y[4];
-            const f32x4 bj = cb(jj);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + bj[r]);
+            for (int r = 0; r < 4; ++r) y[r] = bfr(v[r] + (FULL ? (float)braw[jj][r] : bias[jj][r]));
             if (EPI == EPI_BF16) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) oc[h][r] = f2bf(y[r]);
@@ -683,21 +715,68 @@ __device__ __forceinline__ void epilogue4w(const GemmArgs& g, const f32x4 (&acc)
             } else {    // EPI_RESID: x + y*gate (two roundings, as torch)
 #pragma unroll
               for (int r = 0; r < 4; ++r) ox[h][r] = f2bf(y[r]);
-              const f32x4 res = widen(buf[i][jj]), gj = cg(jj);
+              const f32x4 res = widen(buf[i][jj]);
               f32x4 o;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gj[r]);
-              if (n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
+              for (int r = 0; r < 4; ++r) o[r] = res[r] + mul_rn(y[r], gate[jj][r]);
+              if (SH) *(f32x4*)(wl + ((i & 1) * 16 + (lane & 15)) * RSF + (16 * jj + 4 * gq) * 4) = o;
+              else if (FULL || n < g.N) *(f32x4*)((float*)g.C + (int64_t)m * g.ldc + n) = o;
             }
           }
+          if (SH) {          // bf16 C / aux of this fragment into the pass image
+            const int rr = (i & 1) * 16 + (lane & 15), cb = (16 * jj + 4 * gq) * 2;
+            if (!F32C) *(bf16x4*)(wl + rr * RSB + cb) = oc[h];
+            if (HAS_AUX && g.aux) *(bf16x4*)(wl + AUX0 + rr * RSB + cb) = ox[h];
+          }
         }
-        if (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)
-          st_pair((bf16*)g.C, g.ldc, wide_c, m, j, oc[0], oc[1]);
-        if ((EPI == EPI_GELU || EPI == EPI_RESID) && g.aux)
-          st_pair(g.aux, g.ldaux, wide_x, m, j, ox[0], ox[1]);
+        if (!SH) {
+          if (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)
+            st_pair((bf16*)g.C, g.ldc, wide_c, m, j, oc[0], oc[1]);
+          if ((EPI == EPI_GELU || EPI == EPI_RESID) && g.aux)
+            st_pair(g.aux, g.ldaux, wide_x, m, j, ox[0], ox[1]);
+        }
       }
     }
+    if (SH && (i & 1)) {     // the pass's 32 rows leave row-major: whole cache lines per store
+      wave_lds_sync();
+      const int64_t r0 = (int64_t)(mb - (lane & 15)) + 16 * (i - 1);   // first row of the pass
+      const int c0 = nb - 4 * gq;                                         // the wave's first column
+      if (F32C) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int row = 2 * k + (lane >> 5), c4 = lane & 31;
+          const f32x4 o = *(const f32x4*)(wl + row * RSF + c4 * 16);
+          *(f32x4*)((float*)g.C + (r0 + row) * g.ldc + c0 + 4 * c4) = o;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = 4 * k + (lane >> 4), c8 = lane & 15;
+          const u32x4 o = *(const u32x4*)(wl + row * RSB + c8 * 16);
+          *(u32x4*)((bf16*)g.C + (r0 + row) * g.ldc + c0 + 8 * c8) = o;
+        }
+      }
+      if (HAS_AUX && g.aux) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = 4 * k + (lane >> 4), c8 = lane & 15;
+          const u32x4 o = *(const u32x4*)(wl + AUX0 + row * RSB + c8 * 16);
+          *(u32x4*)(g.aux + (r0 + row) * g.ldaux + c0 + 8 * c8) = o;
+        }
+      }
+      wave_lds_sync();       // the next pass rewrites the image
+    }
   }
+}
+
+// the FULL epilogue's preconditions (uniform per workgroup): the whole 256 x 256 tile in range and
+// every vector access of the FULL path aligned
+__device__ __forceinline__ bool epi4_full(const GemmArgs& g, int m0, int n0, int epi) {
+  const bool bf16_c = epi == EPI_BF16 || epi == EPI_GELU || epi == EPI_DGELU;
+  return m0 + 256 <= g.M && n0 + 256 <= g.N &&
+         (!bf16_c || ((g.ldc % 8) == 0 && (((uintptr_t)g.C) & 15) == 0)) &&
+         (!g.aux || ((g.ldaux % 8) == 0 && (((uintptr_t)g.aux) & 15) == 0)) &&
+         (!g.bias || (((uintptr_t)g.bias) & 7) == 0) && (!g.gate || (((uintptr_t)g.gate) & 15) == 0);
 }
 
 #ifndef GEMM4_PREWAIT
@@ -757,6 +836,10 @@ __device__ __forceinline__ bf16x8 read_frag_a64(const char* slot, int h, int bas
 // phase.  With GEMM4_STAGGER = S > 0 the first-wave workgroup of slot s = (bid >> 3) & 31 on its
 // XCD first waits s/32 * S * K shader cycles (S ~ 54 cycles per K is one tile's main loop at
 // 1.3 PF), so the CUs' epilogues fall at spread-out times from then on.  Grids of >= 2 waves only.
+// Measured (one process, 720p shapes, profiles/r05_ab_gemm_stagger.txt): S = 7 gains 1-2.6 % on
+// the o-projection shape, loses up to 2.1 % on FFN-down and dX, and the dW kernel (K = L) loses
+// 10-17 % to the start delay; larger S lose more.  The epilogue's cost does not follow the
+// chip-wide burst, so the stagger stays off
 #ifndef GEMM4_STAGGER
 #define GEMM4_STAGGER 0
 #endif
@@ -997,14 +1080,23 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // MFMA-write -> v_accvgpr_read distance by hand before the epilogue
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   const int mb = m0 + wm * 128 + (lane & 15), nb = n0 + wn * 128 + 4 * (lane >> 4);
-  if (EPI4_LDSCOEF) {        // every wave's DMA has landed before any wave writes its LDS block
+  const bool full = epi4_full(g, m0, n0, EPI);
+  // the shuffle where it measured faster: the fp32 gated residual (2-3 % over FULL) and dGELU
+  // (0.3-1 %); GELU's two bf16 outputs and the fp32 C without input ran slower through it, the
+  // plain bf16 C tied (profiles/r05_ab_gemm_sh.txt, r05_gemm_epi_probe.txt)
+  constexpr bool SH = EPI4_SHUFFLE && sizeof(smem) >= 4 * EPI4_WLDS && (EPI == EPI_RESID || EPI == EPI_DGELU);
+  if (SH && full) {          // the shuffle images reuse the ring: every wave's DMA has landed
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16))
-    epilogue4w<EPI, true>(g, acc, mb, nb, smem + wid * 1024);
-  else
-    epilogue4w<EPI, false>(g, acc, mb, nb, smem + wid * 1024);
+  char* const wl = smem + wid * EPI4_WLDS;
+  if (EPI == EPI_DGELU || (EPI == EPI_RESID && g.res_bf16)) {
+    if (full) epilogue4w<EPI, true, true, SH>(g, acc, mb, nb, wl);
+    else epilogue4w<EPI, true, false>(g, acc, mb, nb);
+  } else {
+    if (full) epilogue4w<EPI, false, true, SH>(g, acc, mb, nb, wl);
+    else epilogue4w<EPI, false, false>(g, acc, mb, nb);
+  }
 }
 
 // ---------------------------------------- 256x256, four waves, MFMA 32x32x16 (gemm4x) -------

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--shapes", default="qkv,o,ffn1,ffn2")
     ap.add_argument("--passes", default="fwd,dx,dw")
     ap.add_argument("--tiles", default=None, help="per-lib tile codes, comma separated")
+    ap.add_argument("--bias", action="store_true", help="the forward passes on W^T with a bf16 bias (the "
+                    "block's projections all have one)")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else [a.tile] * len(libs)
@@ -52,7 +54,8 @@ def main():
             if pas.endswith("_t"):    # forward passes on the transposed weight (MN-major B)
                 epi = {"fwd_t": 0, "gelu_t": 1, "resid_t": 2}[pas]
                 rc = lib.prfl_gemm_bf16_tiled(x.data_ptr(), K, 1, wt.data_ptr(), N, 0, o.data_ptr(), N, L, N, K,
-                                              epi, None, gate.data_ptr() if epi == 2 else None,
+                                              epi, bias.data_ptr() if a.bias else None,
+                                              gate.data_ptr() if epi == 2 else None,
                                               res.data_ptr() if epi == 2 else None, N, 0,
                                               aux.data_ptr() if epi else None, N, 0, tile_of[id(lib)], st)
                 assert rc == 0, rc
@@ -89,6 +92,7 @@ def main():
             assert rc == 0, rc
 
         gate = torch.randn(N, device=dev, generator=g)
+        bias = (torch.randn(N, device=dev, generator=g) * 0.1).to(torch.bfloat16)
         res = torch.randn(L, N, device=dev, generator=g)
         aux = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
         pre_k = torch.randn(L, K, device=dev, generator=g).to(torch.bfloat16)
