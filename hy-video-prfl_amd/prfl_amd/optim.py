@@ -146,10 +146,12 @@ class AdamW:
         rest = [p for p in model.parameters() if id(p) not in inner]
         order = {id(p): i for i, p in enumerate(rest + [p for g in groups for p in g.parameters()])}
         self.params.sort(key=lambda p: order.get(id(p), len(order)))
-        if self.state and getattr(self, "_host_set", None) is not None:
-            raise RuntimeError("attach() must precede the first step / init_state(): the host-"
-                               "moment tail is chosen in update order")
-        self._host_set = None
+        if self.state and self.state_on_host is not True and self.state_on_host is not False:
+            # a fractional host tail is chosen in update order: its moments must not exist yet
+            raise RuntimeError("attach() must precede the first step / init_state() when "
+                               "state_on_host is a fraction: the host tail is chosen in update order")
+        if not self.state:
+            self._host_set = None
         self._hooks.append(model.register_forward_pre_hook(lambda m, a: self.wait(rest)))
         for g in groups:
             ps = list(g.parameters())
