@@ -61,9 +61,12 @@ def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_h
         if keep_attn:
             aos.append(S["attn"][0])
             lses.append(S["attn"][1])
-    out = torch.stack(outs)
+    # one sample (every PRFL / PAVRM step): a view of the fresh per-sample buffers instead of a
+    # stacked copy (1.5 GB of fp32 per 720p block forward, ~0.3 ms each)
+    cat = (lambda ts: ts[0].unsqueeze(0)) if len(outs) == 1 else torch.stack
+    out = cat(outs)
     if keep_attn:
-        return out, torch.stack(aos), torch.stack(lses)
+        return out, cat(aos), cat(lses)
     return out, _empty(x, BF16), _empty(x, F32)
 
 
@@ -101,8 +104,8 @@ def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, para
         dxs.append(dx)
         des.append(de)
         dcs.append(dc)
-    res = [torch.stack(dxs).to(x.dtype), torch.stack(des),
-           torch.stack(dcs).to(context.dtype) if want_ctx else _empty(context)]
+    cat = (lambda ts: ts[0].unsqueeze(0)) if len(dxs) == 1 else torch.stack
+    res = [cat(dxs).to(x.dtype), cat(des), cat(dcs).to(context.dtype) if want_ctx else _empty(context)]
     for n, p in zip(names, params):
         res.append(G[n].to(p.dtype) if want_w else _empty(p))
     return res
