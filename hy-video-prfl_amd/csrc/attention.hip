@@ -286,6 +286,15 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_SUMCHECK
 #define ATTN_SUMCHECK 1
 #endif
+// wave priorities of the forward's ping-pong: 1 = waves 4-7 at static priority 1 (the lagging
+// half); 0 = none; 2 = each wave at priority 1 through its MFMA phase X and 0 through its
+// softmax phase Y; 3 = the reverse (softmax phase prioritised).  All four within 0.4 % at 720p
+// and 480p (profiles/r05_ab_attn_prio.txt): in-kernel phase cycles (ATTN_PHASETIME) show each
+// wave's 48-MFMA phase at ~1 950 cycles per tile against the 1 536 of its MFMAs alone, whatever
+// the priorities (profiles/r05_attn_fwd_phases.txt)
+#ifndef ATTN_FWD_PRIO
+#define ATTN_FWD_PRIO 1
+#endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
@@ -298,6 +307,22 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // read instructions of the P.V product, the same operand values in the same k-slot order
 // (outputs bit-identical to the row-major path)
 
+// Diagnostic build only (ATTN_PHASETIME=1, never the shipped library): the first 64 workgroups of
+// every long-KV forward launch add, per wave, the shader cycles spent in the X phase (S and P.V
+// MFMAs), its vmcnt wait, the first barrier, the Y phase (softmax), its vmcnt wait and the second
+// barrier into g_attn_phase[wave][6] (vector atomics from lane 0), read by prfl_attn_phase_read.
+#ifndef ATTN_PHASETIME
+#define ATTN_PHASETIME 0
+#endif
+#if ATTN_PHASETIME
+__device__ unsigned long long g_attn_phase[8 * 8];
+__device__ __forceinline__ unsigned phase_clk() {     // shader cycles (s_memtime, low 32 bits)
+  return (unsigned)__builtin_amdgcn_s_memtime();
+}
+#endif
+
+// (Measured and dropped: the O^T accumulators in AGPRs through inline-asm P.V MFMAs -- at two
+// waves per SIMD hipcc then splits the unified register file 128 / 128 and spills 580 B.)
 template <bool SHORT_KV, int SCHED, int NKT, bool QS, bool VT = false>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
@@ -406,15 +431,28 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
   bar();
   if (gp == 1) {          // the lagging (younger) half: one barrier behind, static priority 1
-    __builtin_amdgcn_s_setprio(1);
+    if (SHORT_KV || ATTN_FWD_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     bar();
   }
 
   f32x16 s[NKT];
   bf16x8 pf[NKT][2];
   int st = 0, stp = 2;
+#if ATTN_PHASETIME
+  const bool ptime = !SHORT_KV && blockIdx.x < 64;
+  unsigned ph[6] = {0, 0, 0, 0, 0, 0}, pt0 = phase_clk(), pt1;
+  auto ptick = [&](int k) {
+    pt1 = phase_clk();
+    ph[k] += pt1 - pt0;
+    pt0 = pt1;
+  };
+#define PTICK(k) ptick(k)
+#else
+#define PTICK(k)
+#endif
   for (int t = 0; t <= nkv; ++t) {
     // ---------------- X_t ----------------
+    if (!SHORT_KV && ATTN_FWD_PRIO >= 2) __builtin_amdgcn_s_setprio(ATTN_FWD_PRIO == 2 ? 1 : 0);
     if (!ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
     if (t < nkv) {
       const char* Ks = smem + st * SB;
@@ -462,8 +500,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 1);
       }
     }
+    PTICK(0);
     if (gp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PTICK(1);
     bar();
+    PTICK(2);
+    if (!SHORT_KV && ATTN_FWD_PRIO >= 2) __builtin_amdgcn_s_setprio(ATTN_FWD_PRIO == 2 ? 0 : 1);
     // ---------------- Y_t ----------------
     // (waves 4-7 issuing the whole tile t+2 here, waves 0-3 none: 3.9 % slower, the 12 pieces
     // per wave outgrow the softmax phase; profiles/r03_ab_attn_dma_g1.txt)
@@ -618,11 +660,22 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
       }
       }
     }
+    PTICK(3);
     if (gp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PTICK(4);
     bar();
+    PTICK(5);
     stp = st;
     st = st == 2 ? 0 : st + 1;
   }
+#undef PTICK
+#if ATTN_PHASETIME
+  if (ptime && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_attn_phase[w * 8 + k], (unsigned long long)ph[k]);
+    atomicAdd(&g_attn_phase[w * 8 + 6], 1ull);
+  }
+#endif
   if (gp == 0) bar();
   if (clk) {               // effective shader clock over this workgroup's lifetime (prof.hip)
     const unsigned long long c1 = clock64(), w1 = wall_clock64();
@@ -2219,3 +2272,13 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
                           delta, dq, lddq, bdq, dk, lddk, bdk, dv, lddv, bdv, B, Lq, Lk, H, k_len,
                           scale, nullptr, 0, stream);
 }
+
+#if ATTN_PHASETIME
+// diagnostic build only: the accumulated phase cycles [8 waves][8] (6 phases, workgroup count),
+// then cleared
+extern "C" int prfl_attn_phase_read(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_phase), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
+  static const unsigned long long zero[64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

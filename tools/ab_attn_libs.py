@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="time prfl_attn_fwd_fp8 (config C5) instead")
     ap.add_argument("--qs", default="", help="comma list of lib indices built with ATTN_QS=1: they "
                     "get q pre-scaled by softmax_scale * log2(e) (rounded to bf16 once)")
+    ap.add_argument("--phases", action="store_true", help="libs built with ATTN_PHASETIME=1: after the "
+                    "timing, one more forward and the per-wave phase cycles of its first 64 workgroups")
     ap.add_argument("--vt", default="", help="comma list of lib indices to run through the VT entry "
                     "(prfl_attn_v_to_vt + prfl_attn_fwd_l2q_vt_ws, the transpose inside the timing)")
     a = ap.parse_args()
@@ -143,6 +145,23 @@ def main():
                     errs[i].append(((o - ref).norm() / ref.norm()).item())
             print("fwd rel-L2 vs fp64 (48 rows x 3 heads): " +
                   " | ".join(f"lib{i} {max(e):.2e}" for i, e in enumerate(errs)), flush=True)
+    if a.phases:
+        import ctypes
+        names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y (softmax)", "Y vmcnt", "barrier 2")
+        for i, lib in enumerate(libs):
+            if not hasattr(lib, "prfl_attn_phase_read"):
+                continue
+            buf = (ctypes.c_ulonglong * 64)()
+            lib.prfl_attn_phase_read(buf)          # clear
+            fwd(lib, outs[i])
+            torch.cuda.synchronize()
+            assert lib.prfl_attn_phase_read(buf) == 0
+            for wv in range(8):
+                n = max(buf[wv * 8 + 6], 1)
+                tot = sum(buf[wv * 8 + k] for k in range(6))
+                print(f"lib{i} wave {wv}: " + ", ".join(f"{names[k]} {buf[wv * 8 + k] / n / 1e3:.1f}k "
+                      f"({100 * buf[wv * 8 + k] / max(tot, 1):.1f}%)" for k in range(6))
+                      + f" | {n} workgroups", flush=True)
 
 
 if __name__ == "__main__":
