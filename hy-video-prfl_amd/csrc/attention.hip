@@ -280,6 +280,9 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // scores instead of one per score; the pair is folded once per tile).  Measured 11.7 % SLOWER at
 // 720p (85.14 -> 95.14 ms) and 10.1 % at 480p, same error vs fp64 (profiles/r05_ab_attn_pksum.txt):
 // packed f32 beside MFMAs costs far more than its issue slot (MI355X guide, constants table).  Off
+#ifndef ATTN_ROWSUM_CHAINS
+#define ATTN_ROWSUM_CHAINS 1
+#endif
 #ifndef ATTN_PKSUM
 #define ATTN_PKSUM 0
 #endif
@@ -295,6 +298,34 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_FWD_PRIO
 #define ATTN_FWD_PRIO 1
 #endif
+// PVFIRST (VT, q in log2 units, long KV): the X phase issues P(t-1).V first and S(t) second as ONE
+// scheduling region (both unconditional: S(nkv) computes on a stale stage and is never used,
+// P(-1).V multiplies zeros -- pf = 0 and stage 2's V image zeroed -- so O is unchanged bit for
+// bit), with the LDS reads 4 MFMAs ahead across the P.V -> S seam, and the first 4 V^T fragments
+// of P(t).V read at the END of Y_t, before the barrier (V(t) has been visible since X_t; nothing
+// writes its stage before X_{t+2}).  Phase cycles (ATTN_PHASETIME, profiles/r05_attn_fwd_phases.txt)
+// put each 48-MFMA phase ~400 cycles over its MFMAs with an idle partner: the two region starts
+// (S, then P.V) each waited out an LDS read latency.
+#ifndef ATTN_FWD_PVFIRST
+#define ATTN_FWD_PVFIRST 0
+#endif
+// KDMA_X (with PVFIRST): each wave issues the K pieces of the tile it loads one phase earlier, in
+// its MFMA phase X, and only the V pieces in its softmax phase Y (waves 0-3: K(t+1) in X_t, V(t+1)
+// in Y_t; waves 4-7: K(t+2) in X_t, V(t+2) in Y_t).  An LDS-DMA piece holds its wave for ~100
+// cycles of issue: the 6 pieces per tile were ~600 of the ~2 100 cycles of the softmax phase, the
+// critical one once PVFIRST trimmed X (profiles/r05_attn_fwd_phases.txt).  K(T)'s stage held
+// tile T-3, whose K was last read by S(T-3) in X_{T-3} or the rare recompute in Y_{T-3}: both
+// before the barrier that opens the issuing X phase; K(T) is retired by the issuing wave's vmcnt
+// before the barrier that ends that X phase, ahead of S(T).
+#ifndef ATTN_FWD_KDMA_X
+#define ATTN_FWD_KDMA_X 0
+#endif
+// the wave's K (and V) pieces of a tile under ONE m0 write (consecutive KiB of LDS, piece i at
+// instruction offset i KiB, pre-subtracted from its per-lane source offset) instead of a save /
+// set / s_nop / restore of m0 around every piece
+#ifndef ATTN_FWD_DMA_GROUPED
+#define ATTN_FWD_DMA_GROUPED 0
+#endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
 #endif
@@ -309,10 +340,14 @@ __device__ __forceinline__ float xhalf_max(float x) {
 
 // Diagnostic build only (ATTN_PHASETIME=1, never the shipped library): the first 64 workgroups of
 // every long-KV forward launch add, per wave, the shader cycles spent in the X phase (S and P.V
-// MFMAs), its vmcnt wait, the first barrier, the Y phase (softmax), its vmcnt wait and the second
-// barrier into g_attn_phase[wave][6] (vector atomics from lane 0), read by prfl_attn_phase_read.
+// MFMAs), its vmcnt wait, the first barrier, the Y phase's softmax, its vmcnt wait, the second
+// barrier and the Y phase's DMA issue into g_attn_phase[wave][0..6] (slot 7: workgroups; vector
+// atomics from lane 0), read by prfl_attn_phase_read.
 #ifndef ATTN_PHASETIME
 #define ATTN_PHASETIME 0
+#endif
+#ifndef ATTN_PHASE_SOLO
+#define ATTN_PHASE_SOLO 0
 #endif
 #if ATTN_PHASETIME
 __device__ unsigned long long g_attn_phase[8 * 8];
@@ -328,6 +363,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TK = NKT * 32;                 // keys per tile
   constexpr int SV = NKT * 8192;               // bytes of one K (or V) tile image
   constexpr int SB = 2 * SV;                   // bytes of one [K | V] ring stage
+  constexpr bool DMAG = ATTN_FWD_DMA_GROUPED && NKT <= 4;
   __shared__ __attribute__((aligned(16))) char smem[3 * SB];   // ring of [K | V] tiles
   // unit = (sample, head, query tile); the last units of the grid are split over `split`
   // workgroups that each take a contiguous share of the key tiles (the final dispatch round
@@ -406,26 +442,55 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     vov[i] = VT ? (uint32_t)((w * NKT + i) * 1024 + lane * 16)       // contiguous, lane-linear
                 : (uint32_t)(row * a.ldv * 2) + ((pc ^ swzb) << 4);
   }
-  auto dma = [&](int t, int st) {      // local tile t = key tile t0 + t
+  // this wave's K pieces (part 1), V pieces (part 2) or both (3) of local tile t = key tile t0 + t
+  auto dma_parts = [&](int t, int st, int parts) {
     char* Ks = smem + st * SB;
     char* Vs = Ks + SV;
     const int tg = t0 + t;
     const int rows = min(a.Lk - tg * TK, TK);
-    const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
-    const i32x4 sv = VT ? make_srd(Vb + (int64_t)tg * TK * HD, (uint32_t)SV)
-                        : make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
+    if (parts & 1) {
+      const i32x4 sk = make_srd(Kb + (int64_t)tg * TK * a.ldk, (uint32_t)(rows * a.ldk * 2));
+      if (DMAG) {        // one m0 for the wave's NKT consecutive KiB (piece i: instruction offset)
+        unsigned keep;
+        m0_set(lds_addr(Ks + w * NKT * 1024), keep);
 #pragma unroll
-    for (int i = 0; i < NKT; ++i) {
-      dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
-      dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
+        for (int i = 0; i < NKT; ++i) dma16_buf_m0(sk, vok[i] - i * 1024, 0, i);
+        m0_restore(keep);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NKT; ++i) dma16_buf(sk, vok[i], 0, lds_addr(Ks + (w * NKT + i) * 1024));
+      }
+    }
+    if (parts & 2) {
+      const i32x4 sv = VT ? make_srd(Vb + (int64_t)tg * TK * HD, (uint32_t)SV)
+                          : make_srd(Vb + (int64_t)tg * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
+      if (DMAG) {
+        unsigned keep;
+        m0_set(lds_addr(Vs + w * NKT * 1024), keep);
+#pragma unroll
+        for (int i = 0; i < NKT; ++i) dma16_buf_m0(sv, vov[i] - i * 1024, 0, i);
+        m0_restore(keep);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NKT; ++i) dma16_buf(sv, vov[i], 0, lds_addr(Vs + (w * NKT + i) * 1024));
+      }
     }
   };
+  auto dma = [&](int t, int st) { dma_parts(t, st, 3); };
   auto bar = [&]() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
+  constexpr bool PVF = ATTN_FWD_PVFIRST && VT && QS && !SHORT_KV;
+  constexpr bool KDX = PVF && ATTN_FWD_KDMA_X && ATTN_G0_DMA_Y;
+  if (PVF) {              // stage 2's V image = zeros for the t = 0 P(-1).V (retired by the barrier)
+    static_assert(!PVF || SV % (512 * 16) == 0, "zeroing stride");
+#pragma unroll
+    for (int i = 0; i < SV / (512 * 16); ++i)
+      *(u32x4*)(smem + 2 * SB + SV + (i * 512 + tid) * 16) = (u32x4){0u, 0u, 0u, 0u};
+  }
   if (nkv > 0) dma(0, 0);
   if (nkv > 1) dma(1, 1);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
@@ -438,9 +503,21 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   f32x16 s[NKT];
   bf16x8 pf[NKT][2];
   int st = 0, stp = 2;
+  // PVF: the V^T fragment i of P.V in stage `stg` (i: dt = i / 2NKT, kt = (i / 2) % NKT, s2 = i & 1)
+  auto vfrag = [&](int stg, int i) {
+    const int dt = i / (2 * NKT), kt = (i >> 1) % NKT, s2 = i & 1;
+    return *(const bf16x8*)(smem + stg * SB + SV + (kt * 4 + 2 * s2) * 2048 + vtoff[dt]);
+  };
+  bf16x8 vpre[4];
+  if (PVF) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) pf[kt][0] = pf[kt][1] = (bf16x8){};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vpre[i] = (bf16x8){};
+  }
 #if ATTN_PHASETIME
   const bool ptime = !SHORT_KV && blockIdx.x < 64;
-  unsigned ph[6] = {0, 0, 0, 0, 0, 0}, pt0 = phase_clk(), pt1;
+  unsigned ph[7] = {0, 0, 0, 0, 0, 0, 0}, pt0 = phase_clk(), pt1;
   auto ptick = [&](int k) {
     pt1 = phase_clk();
     ph[k] += pt1 - pt0;
@@ -454,7 +531,39 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     // ---------------- X_t ----------------
     if (!SHORT_KV && ATTN_FWD_PRIO >= 2) __builtin_amdgcn_s_setprio(ATTN_FWD_PRIO == 2 ? 1 : 0);
     if (!ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-    if (t < nkv) {
+    if (KDX) {            // the K pieces of this wave's next tile (V follows in Y)
+      if (gp == 0 && t + 1 < nkv) dma_parts(t + 1, st == 2 ? 0 : st + 1, 1);
+      if (gp == 1 && t + 2 < nkv) dma_parts(t + 2, stp, 1);
+    }
+    if (PVF && !(ATTN_PHASE_SOLO == 3 && gp == 1)) {
+      constexpr int NP = 8 * NKT, NX = 2 * NP;          // 24 P.V then 24 S MFMAs
+      const char* Ks = smem + st * SB;
+      auto frag = [&](int i) {
+        if (i < NP) return vfrag(stp, i);
+        const int j = i - NP;
+        return *(const bf16x8*)(Ks + (j >> 3) * 8192 + koff[j & 7]);
+      };
+      bf16x8 ring[5];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        if (i + 4 < NX) ring[(i + 4) % 5] = frag(i + 4);
+        const bf16x8 f = i < 4 ? vpre[i] : ring[i % 5];
+        if (i < NP) {
+          const int dt = i / (2 * NKT), kt = (i >> 1) % NKT, s2 = i & 1;
+          o[dt] = mfma32(f, pf[kt][s2], o[dt]);
+        } else {
+          const int j = i - NP, kt = j >> 3, ks = j & 7;
+          s[kt] = mfma32(f, qf[ks], ks == 0 ? negm : s[kt]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NX - 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    if (!PVF && t < nkv) {
       const char* Ks = smem + st * SB;
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
@@ -475,7 +584,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, SCHED + 1, 0);
       }
     }
-    if (t > 0) {
+    if (!PVF && t > 0) {
       const char* Vs = smem + stp * SB;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -509,9 +618,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
     // ---------------- Y_t ----------------
     // (waves 4-7 issuing the whole tile t+2 here, waves 0-3 none: 3.9 % slower, the 12 pieces
     // per wave outgrow the softmax phase; profiles/r03_ab_attn_dma_g1.txt)
-    if (gp == 1 && t + 2 < nkv) dma(t + 2, stp);
-    if (ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma(t + 1, st == 2 ? 0 : st + 1);
-    if (t < nkv) {
+    if (gp == 1 && t + 2 < nkv) dma_parts(t + 2, stp, KDX ? 2 : 3);
+    if (ATTN_G0_DMA_Y && gp == 0 && t + 1 < nkv) dma_parts(t + 1, st == 2 ? 0 : st + 1, KDX ? 2 : 3);
+    PTICK(6);
+    // (diagnostic builds only, wrong results: ATTN_PHASE_SOLO 1 / 2 = waves 0-3 / 4-7 skip their
+    // softmax, so the other half's MFMA phase runs beside an idle partner; 3 = waves 4-7 skip
+    // their MFMA phase (PVFIRST), so waves 0-3's softmax runs beside an idle partner)
+    if (t < nkv && !(ATTN_PHASE_SOLO == 1 + gp)) {
       const int kbase = (t0 + t) * TK;
       auto mask_tail = [&]() {
         if (kbase + TK > a.k_len) {
@@ -552,6 +665,23 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
                 t2 += p;
               }
             ts = t2[0] + t2[1];
+          } else if (ATTN_ROWSUM_CHAINS > 1) {
+            // the tile sum as ATTN_ROWSUM_CHAINS interleaved partial sums: the 48-add dependency
+            // chain was the softmax phase's critical path (profiles/r05_attn_fwd_phases.txt)
+            constexpr int NC = ATTN_ROWSUM_CHAINS;
+            float tc[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) tc[c] = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kt][r]);
+                s[kt][r] = p;
+                tc[(kt * 16 + r) % NC] += p;
+              }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) ts += tc[c];
           } else {
 #pragma unroll
             for (int kt = 0; kt < NKT; ++kt)
@@ -631,6 +761,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
                                   f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
                                   f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
                                   f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+        if (PVF) {       // the first V^T fragments of P(t).V in X_{t+1}, read before the barrier
+#pragma unroll
+          for (int i = 0; i < 4; ++i) vpre[i] = vfrag(st, i);
+        }
       } else {
       const float mx = row_max();
       const float mnew = fmaxf(m, mx * a.sl2);
@@ -672,8 +806,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #if ATTN_PHASETIME
   if (ptime && lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_attn_phase[w * 8 + k], (unsigned long long)ph[k]);
-    atomicAdd(&g_attn_phase[w * 8 + 6], 1ull);
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_attn_phase[w * 8 + k], (unsigned long long)ph[k]);
+    atomicAdd(&g_attn_phase[w * 8 + 7], 1ull);
   }
 #endif
   if (gp == 0) bar();

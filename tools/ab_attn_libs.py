@@ -147,7 +147,8 @@ def main():
                   " | ".join(f"lib{i} {max(e):.2e}" for i, e in enumerate(errs)), flush=True)
     if a.phases:
         import ctypes
-        names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y (softmax)", "Y vmcnt", "barrier 2")
+        names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y softmax", "Y vmcnt", "barrier 2",
+                 "Y DMA issue")
         for i, lib in enumerate(libs):
             if not hasattr(lib, "prfl_attn_phase_read"):
                 continue
@@ -157,10 +158,10 @@ def main():
             torch.cuda.synchronize()
             assert lib.prfl_attn_phase_read(buf) == 0
             for wv in range(8):
-                n = max(buf[wv * 8 + 6], 1)
-                tot = sum(buf[wv * 8 + k] for k in range(6))
+                n = max(buf[wv * 8 + 7], 1)
+                tot = sum(buf[wv * 8 + k] for k in range(7))
                 print(f"lib{i} wave {wv}: " + ", ".join(f"{names[k]} {buf[wv * 8 + k] / n / 1e3:.1f}k "
-                      f"({100 * buf[wv * 8 + k] / max(tot, 1):.1f}%)" for k in range(6))
+                      f"({100 * buf[wv * 8 + k] / max(tot, 1):.1f}%)" for k in range(7))
                       + f" | {n} workgroups", flush=True)
 
 
