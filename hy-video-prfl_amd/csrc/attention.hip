@@ -305,9 +305,12 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // of P(t).V read at the END of Y_t, before the barrier (V(t) has been visible since X_t; nothing
 // writes its stage before X_{t+2}).  Phase cycles (ATTN_PHASETIME, profiles/r05_attn_fwd_phases.txt)
 // put each 48-MFMA phase ~400 cycles over its MFMAs with an idle partner: the two region starts
-// (S, then P.V) each waited out an LDS read latency.
+// (S, then P.V) each waited out an LDS read latency.  With PVFIRST the MFMA phase runs at ~1 650
+// cycles per tile (1 536 of MFMAs) and the softmax phase (~1 300 cycles of VALU + ~600 of LDS-DMA
+// issue) is the critical one; bit-identical, 0.5-1.2 % faster at 720p / 480p / C1 over five
+// one-process A/Bs (profiles/r05_ab_attn_pvfirst.txt)
 #ifndef ATTN_FWD_PVFIRST
-#define ATTN_FWD_PVFIRST 0
+#define ATTN_FWD_PVFIRST 1
 #endif
 // KDMA_X (with PVFIRST): each wave issues the K pieces of the tile it loads one phase earlier, in
 // its MFMA phase X, and only the V pieces in its softmax phase Y (waves 0-3: K(t+1) in X_t, V(t+1)
@@ -341,16 +344,39 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // Diagnostic build only (ATTN_PHASETIME=1, never the shipped library): the first 64 workgroups of
 // every long-KV forward launch add, per wave, the shader cycles spent in the X phase (S and P.V
 // MFMAs), its vmcnt wait, the first barrier, the Y phase's softmax, its vmcnt wait, the second
-// barrier and the Y phase's DMA issue into g_attn_phase[wave][0..6] (slot 7: workgroups; vector
-// atomics from lane 0), read by prfl_attn_phase_read.
+// barrier, the Y phase's DMA issue, its exp / sum / check and its P packing into
+// g_attn_phase[wave][0..8] (slot 15: workgroups; vector atomics from lane 0), read by
+// prfl_attn_phase_read.
 #ifndef ATTN_PHASETIME
 #define ATTN_PHASETIME 0
 #endif
 #ifndef ATTN_PHASE_SOLO
 #define ATTN_PHASE_SOLO 0
 #endif
+#ifndef ATTN_DIAG_SOFTMAX
+#define ATTN_DIAG_SOFTMAX 0
+#endif
+// EXP_POLY = k: the forward's exp2 of the last k key sub-tiles (of NKT) on the FMA pipe instead of
+// the transcendental unit: 2^x = 2^floor(x) * q(x - floor(x)), q a degree-4 minimax polynomial on
+// [0, 1) (rel. error < 4e-6, far below the bf16 rounding of P), x clamped at -126 (2^-126 for
+// the masked -inf scores: 1e-38 beside a row maximum of 1)
+#ifndef ATTN_EXP_POLY
+#define ATTN_EXP_POLY 0
+#endif
+__device__ __forceinline__ float exp2_poly(float x) {
+  x = fmaxf(x, -126.f);
+  const float xi = __builtin_floorf(x);
+  const float f = x - xi;
+  float q = 1.3333558146e-3f;
+  q = __builtin_fmaf(q, f, 9.6181291076e-3f);
+  q = __builtin_fmaf(q, f, 5.5504108665e-2f);
+  q = __builtin_fmaf(q, f, 2.4022650696e-1f);
+  q = __builtin_fmaf(q, f, 6.9314718056e-1f);
+  q = __builtin_fmaf(q, f, 1.0f);
+  return __builtin_ldexpf(q, (int)xi);
+}
 #if ATTN_PHASETIME
-__device__ unsigned long long g_attn_phase[8 * 8];
+__device__ unsigned long long g_attn_phase[8 * 16];
 __device__ __forceinline__ unsigned phase_clk() {     // shader cycles (s_memtime, low 32 bits)
   return (unsigned)__builtin_amdgcn_s_memtime();
 }
@@ -517,7 +543,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   }
 #if ATTN_PHASETIME
   const bool ptime = !SHORT_KV && blockIdx.x < 64;
-  unsigned ph[7] = {0, 0, 0, 0, 0, 0, 0}, pt0 = phase_clk(), pt1;
+  unsigned ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, pt0 = phase_clk(), pt1;
   auto ptick = [&](int k) {
     pt1 = phase_clk();
     ph[k] += pt1 - pt0;
@@ -667,7 +693,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
             ts = t2[0] + t2[1];
           } else if (ATTN_ROWSUM_CHAINS > 1) {
             // the tile sum as ATTN_ROWSUM_CHAINS interleaved partial sums: the 48-add dependency
-            // chain was the softmax phase's critical path (profiles/r05_attn_fwd_phases.txt)
+            // chain was the softmax phase's critical path -- without the sum the exp / sum section
+            // runs in half the cycles (profiles/r05_attn_fwd_phases.txt)
+            // (built with -fno-slp-vectorize: else hipcc packs two chains into v_pk_add_f32, which
+            // costs far more than two adds beside the partner's MFMAs -- the slower ATTN_PKSUM)
             constexpr int NC = ATTN_ROWSUM_CHAINS;
             float tc[NC];
 #pragma unroll
@@ -687,9 +716,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
             for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(s[kt][r]);
+                // (diagnostic builds only, wrong results: ATTN_DIAG_SOFTMAX 1 = no row sum,
+                // 2 = a multiply instead of the v_exp)
+                const float p = ATTN_DIAG_SOFTMAX == 2 ? s[kt][r] * 0.5f
+                              : (kt >= NKT - ATTN_EXP_POLY) ? exp2_poly(s[kt][r]) : __builtin_amdgcn_exp2f(s[kt][r]);
                 s[kt][r] = p;
-                ts += p;
+                if (ATTN_DIAG_SOFTMAX != 1) ts += p;
               }
           }
           if (__any(!(ts <= (float)(1 << ATTN_LAZY_TAU)))) {
@@ -753,6 +785,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
         }
       }
       if (QS) {
+        PTICK(7);
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
@@ -761,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
                                   f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
                                   f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
                                   f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+        PTICK(8);
         if (PVF) {       // the first V^T fragments of P(t).V in X_{t+1}, read before the barrier
 #pragma unroll
           for (int i = 0; i < 4; ++i) vpre[i] = vfrag(st, i);
@@ -806,8 +840,8 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #if ATTN_PHASETIME
   if (ptime && lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 7; ++k) atomicAdd(&g_attn_phase[w * 8 + k], (unsigned long long)ph[k]);
-    atomicAdd(&g_attn_phase[w * 8 + 7], 1ull);
+    for (int k = 0; k < 9; ++k) atomicAdd(&g_attn_phase[w * 16 + k], (unsigned long long)ph[k]);
+    atomicAdd(&g_attn_phase[w * 16 + 15], 1ull);
   }
 #endif
   if (gp == 0) bar();
@@ -2408,11 +2442,11 @@ extern "C" int prfl_attn_bwd(const void* q, int64_t ldq, int64_t bq, const void*
 }
 
 #if ATTN_PHASETIME
-// diagnostic build only: the accumulated phase cycles [8 waves][8] (6 phases, workgroup count),
-// then cleared
+// diagnostic build only: the accumulated phase cycles [8 waves][16] (9 phases, slot 15 the
+// workgroup count), then cleared
 extern "C" int prfl_attn_phase_read(unsigned long long* host) {
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_phase), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
-  static const unsigned long long zero[64] = {};
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_phase), sizeof(unsigned long long) * 128) != hipSuccess) return -1;
+  static const unsigned long long zero[128] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -147,21 +147,21 @@ def main():
                   " | ".join(f"lib{i} {max(e):.2e}" for i, e in enumerate(errs)), flush=True)
     if a.phases:
         import ctypes
-        names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y softmax", "Y vmcnt", "barrier 2",
-                 "Y DMA issue")
+        names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y prefetch+tail", "Y vmcnt", "barrier 2",
+                 "Y DMA issue", "Y mask/exp/sum", "Y pack")
         for i, lib in enumerate(libs):
             if not hasattr(lib, "prfl_attn_phase_read"):
                 continue
-            buf = (ctypes.c_ulonglong * 64)()
+            buf = (ctypes.c_ulonglong * 128)()
             lib.prfl_attn_phase_read(buf)          # clear
             fwd(lib, outs[i])
             torch.cuda.synchronize()
             assert lib.prfl_attn_phase_read(buf) == 0
             for wv in range(8):
-                n = max(buf[wv * 8 + 7], 1)
-                tot = sum(buf[wv * 8 + k] for k in range(7))
-                print(f"lib{i} wave {wv}: " + ", ".join(f"{names[k]} {buf[wv * 8 + k] / n / 1e3:.1f}k "
-                      f"({100 * buf[wv * 8 + k] / max(tot, 1):.1f}%)" for k in range(7))
+                n = max(buf[wv * 16 + 15], 1)
+                tot = sum(buf[wv * 16 + k] for k in range(9))
+                print(f"lib{i} wave {wv}: " + ", ".join(f"{names[k]} {buf[wv * 16 + k] / n / 1e3:.1f}k "
+                      f"({100 * buf[wv * 16 + k] / max(tot, 1):.1f}%)" for k in range(9))
                       + f" | {n} workgroups", flush=True)
 
 
