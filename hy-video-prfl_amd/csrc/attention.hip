@@ -283,6 +283,17 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #ifndef ATTN_ROWSUM_CHAINS
 #define ATTN_ROWSUM_CHAINS 1
 #endif
+// SPEC_PACK (exp-first path): P(t) is taken as it stands -- packed to bf16, its sum added, the
+// first V^T fragments read -- and the branch on the tile sum's overflow check comes only after
+// that; on the rare overflow the row sum is restored, S' recomputed and the max-first path run.
+// With the branch straight after the exps, the 48-add chain and the conversions sat in two basic
+// blocks: the branch waited the chain out.  A diagnostic build without the check ran the whole
+// forward 7 % faster (profiles/r05_attn_fwd_phases.txt).  Same values either way: bit-identical.
+// Measured 2.1 % faster at 720p and 480p, outputs identical (profiles/r05_ab_attn_specpack.txt);
+// it also ends the 12 B spill of the VT = false builds.
+#ifndef ATTN_SPEC_PACK
+#define ATTN_SPEC_PACK 1
+#endif
 #ifndef ATTN_PKSUM
 #define ATTN_PKSUM 0
 #endif
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 
   constexpr bool PVF = ATTN_FWD_PVFIRST && VT && QS && !SHORT_KV;
   constexpr bool KDX = PVF && ATTN_FWD_KDMA_X && ATTN_G0_DMA_Y;
+  constexpr bool SPECPACK = ATTN_SPEC_PACK && QS && ATTN_SUMCHECK;
   if (PVF) {              // stage 2's V image = zeros for the t = 0 P(-1).V (retired by the barrier)
     static_assert(!PVF || SV % (512 * 16) == 0, "zeroing stride");
 #pragma unroll
@@ -533,6 +545,17 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   auto vfrag = [&](int stg, int i) {
     const int dt = i / (2 * NKT), kt = (i >> 1) % NKT, s2 = i & 1;
     return *(const bf16x8*)(smem + stg * SB + SV + (kt * 4 + 2 * s2) * 2048 + vtoff[dt]);
+  };
+  // P(t) packed to bf16 for the P.V MFMAs
+  auto pack_p = [&]() {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
+                              f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
+                              f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
+                              f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
   };
   bf16x8 vpre[4];
   if (PVF) {
@@ -669,8 +692,21 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
         return xhalf_max(mx);
       };
+      // S' recomputed from the still-staged K(t)
+      auto recompute_s = [&]() {
+        const char* Ks = smem + st * SB;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], negm);
+#pragma unroll
+          for (int ks = 1; ks < 8; ++ks)
+            s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
+        }
+        mask_tail();
+      };
       mask_tail();
-      bool max_first = true;
+      bool max_first = true, ovf = false;
+      float lsum0 = 0.f;
       if (QS && ATTN_SUMCHECK) {
         // optimistic: P = exp2(S') against the current max, its tile sum tells whether every P
         // stayed <= 2^TAU (the lazy-rescale bound) without the max pass; else (rare: the row max
@@ -717,30 +753,28 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
                 // (diagnostic builds only, wrong results: ATTN_DIAG_SOFTMAX 1 = no row sum,
-                // 2 = a multiply instead of the v_exp)
+                // 2 = a multiply instead of the v_exp, 3 = no overflow check of the tile sum)
                 const float p = ATTN_DIAG_SOFTMAX == 2 ? s[kt][r] * 0.5f
                               : (kt >= NKT - ATTN_EXP_POLY) ? exp2_poly(s[kt][r]) : __builtin_amdgcn_exp2f(s[kt][r]);
                 s[kt][r] = p;
                 if (ATTN_DIAG_SOFTMAX != 1) ts += p;
               }
           }
-          if (__any(!(ts <= (float)(1 << ATTN_LAZY_TAU)))) {
-            const char* Ks = smem + st * SB;
-#pragma unroll
-            for (int kt = 0; kt < NKT; ++kt) {
-              s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[0]), qf[0], negm);
-#pragma unroll
-              for (int ks = 1; ks < 8; ++ks)
-                s[kt] = mfma32(*(const bf16x8*)(Ks + kt * 8192 + koff[ks]), qf[ks], s[kt]);
-            }
-            mask_tail();
+          if (SPECPACK) {
+            // speculative: taken as it stands, the check's branch comes after the pack and the
+            // first V^T reads below (see ATTN_SPEC_PACK)
+            ovf = ATTN_DIAG_SOFTMAX != 3 && __any(!(ts <= (float)(1 << ATTN_LAZY_TAU)));
+            lsum0 = lsum;
+            lsum += ts;
+          } else if (ATTN_DIAG_SOFTMAX != 3 && __any(!(ts <= (float)(1 << ATTN_LAZY_TAU)))) {
+            recompute_s();
             max_first = true;
           } else {
             lsum += ts;
           }
         }
       }
-      if (QS && max_first) {         // s = S' = S * sl2 - m already
+      auto max_first_path = [&]() {  // s = S' = S * sl2 - m already
         const float mx = row_max();
         // fresh: no tile of this row processed yet (m = -inf, negm = 0: s = S); m is the same in
         // both lane halves of a query (their partial row sums are not: one half's can underflow
@@ -783,21 +817,21 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
               lsum += p;
             }
         }
-      }
+      };
+      if (QS && max_first) max_first_path();
       if (QS) {
         PTICK(7);
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-            pf[kt][s2] = (bf16x8){f2bf(s[kt][8 * s2 + 0]), f2bf(s[kt][8 * s2 + 1]),
-                                  f2bf(s[kt][8 * s2 + 2]), f2bf(s[kt][8 * s2 + 3]),
-                                  f2bf(s[kt][8 * s2 + 4]), f2bf(s[kt][8 * s2 + 5]),
-                                  f2bf(s[kt][8 * s2 + 6]), f2bf(s[kt][8 * s2 + 7])};
+        pack_p();
         PTICK(8);
         if (PVF) {       // the first V^T fragments of P(t).V in X_{t+1}, read before the barrier
 #pragma unroll
           for (int i = 0; i < 4; ++i) vpre[i] = vfrag(st, i);
+        }
+        if (SPECPACK && ovf) {        // (rare) the speculative P(t) overflowed: redo it max-first
+          lsum = lsum0;
+          recompute_s();
+          max_first_path();
+          pack_p();
         }
       } else {
       const float mx = row_max();
