@@ -815,6 +815,11 @@ __device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
 #define GEMM4_A64 1
 #endif
 constexpr int A64SLOT = 32768;
+// diagnostic builds only (wrong results): the A64 loop without its barrier (1), its LDS-DMA and
+// vmcnt waits (2), its fragment reads (4), its vmcnt waits only (8)
+#ifndef GEMM4_DIAG
+#define GEMM4_DIAG 0
+#endif
 
 // byte offset of this lane's 16 B in A piece i (< 4) of half 0 of the wave's 64 rows of a 64-deep
 // slice at k0 = 0 (half 1 = rows + 32: the same lane offsets plus a wave-uniform soffset)
@@ -990,8 +995,8 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
   // slot (j+1) & 3) || DMA of half hh of A slice J into the slot at sa and of B sub-slice j+3
   auto step64 = [&](int j, bf16x8 (&ca)[8], bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8],
                     char* sa, int J, int hh, const char* ra, int hr) {
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own pieces of sub-slice j+1 landed
-    __builtin_amdgcn_s_barrier();
+    if (!(GEMM4_DIAG & 10)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // own pieces of sub-slice j+1 landed
+    if (!(GEMM4_DIAG & 1)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int jb = min(j + 3, ns - 1);
     char* sb = smB + ((j + 3) & 3) * HALF4;
@@ -999,15 +1004,17 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       mfma16(acc[i][0], cb[0], ca[i]);
-      if (i < 4) piece_a64(i, J, hh, sa);
-      else piece_b(i - 4, jb, sb);
+      if (!(GEMM4_DIAG & 2)) {
+        if (i < 4) piece_a64(i, J, hh, sa);
+        else piece_b(i - 4, jb, sb);
+      }
       mfma16(acc[i][1], cb[1], ca[i]);
       __builtin_amdgcn_sched_barrier(0);
-      na[i] = read_frag_a64(ra, hr, wm * 128 + i * 16, lane);
+      na[i] = (GEMM4_DIAG & 4) ? ca[i] : read_frag_a64(ra, hr, wm * 128 + i * 16, lane);
       __builtin_amdgcn_sched_barrier(0);
       mfma16(acc[i][2], cb[2], ca[i]);
       __builtin_amdgcn_sched_barrier(0);
-      nb[i] = read_frag4<B_KC>(rb, wn * 128 + i * 16, lane);
+      nb[i] = (GEMM4_DIAG & 4) ? cb[i] : read_frag4<B_KC>(rb, wn * 128 + i * 16, lane);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int jj = 3; jj < 8; ++jj) mfma16(acc[i][jj], cb[jj], ca[i]);
