@@ -817,6 +817,14 @@ __device__ __forceinline__ void mfma16(f32x4& acc, bf16x8 b, bf16x8 a) {
 constexpr int A64SLOT = 32768;
 // diagnostic builds only (wrong results): the A64 loop without its barrier (1), its LDS-DMA and
 // vmcnt waits (2), its fragment reads (4), its vmcnt waits only (8)
+// (Measured and dropped: B fragments of the next sub-slice read in the step's first half, A in its
+// second -- chunk 0 of a step consumes every B fragment -- tied or lost up to 2 %,
+// profiles/r05_ab_gemm_rorder.txt.)
+// (Measured and dropped, profiles/r05_ab_gemm_dpos.txt: each wave issuing its LDS-DMA piece at a
+// different MFMA gap of the chunk -- after MFMA {0, 3, 5, 7}[wave] or 2 x wave -- so the four
+// waves' pieces do not reach the texture-address unit together: 0.5-2.5 % slower.  A build without
+// the DMA runs 14 % faster and one without its vmcnt waits no faster (profiles/r05_ab_gemm_diag.txt):
+// what the pieces cost is neither the data's arrival nor the four waves' collision.)
 #ifndef GEMM4_DIAG
 #define GEMM4_DIAG 0
 #endif
