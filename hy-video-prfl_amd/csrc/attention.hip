@@ -290,7 +290,10 @@ __device__ __forceinline__ float xhalf_max(float x) {
 // blocks: the branch waited the chain out.  A diagnostic build without the check ran the whole
 // forward 7 % faster (profiles/r05_attn_fwd_phases.txt).  Same values either way: bit-identical.
 // Measured 2.1 % faster at 720p and 480p, outputs identical (profiles/r05_ab_attn_specpack.txt);
-// it also ends the 12 B spill of the VT = false builds.
+// it also ends the 12 B spill of the VT = false builds.  On top of it a build without the overflow
+// check runs only 0.65 % faster, one without the tile sum 3.2 % (profiles/r05_ab_attn_diag_spec.txt);
+// (measured and dropped: that sum taken from the packed P by v_dot2c_f32_bf16 against ones, 24 ops
+// instead of 48 adds -- hipcc then spills 400-550 B.)
 #ifndef ATTN_SPEC_PACK
 #define ATTN_SPEC_PACK 1
 #endif
