@@ -553,10 +553,13 @@ def test_toy_pavrm_steps_vs_reference(golden):
         assert len(ours) > 30
         med = lambda d: sorted(d.values())[len(d) // 2]  # noqa: E731
         worst = sorted(ours.items(), key=lambda kv: -kv[1])[:5]
-        # ours within 5 % of the reference's own median distance (both are bf16 draws around the
-        # truth at ~7 %: round 3's log2-q attention moved ours from just under the reference's to
-        # 1.0001 x it; a broken kernel lands at many x)
-        assert med(ours) <= 1.05 * med(refs), (s, med(ours), med(refs), worst)
+        # ours within 1 % of the reference's own median distance (both are bf16 draws around the
+        # truth at ~7 %; round 5 measured ratio 1.0002 at step 0 and 0.073 at step 1, where the
+        # reference's own run sits 14 % off the truth; the kernels are deterministic, so the gate
+        # was tightened from round 3's 1.05; a broken kernel lands at many x)
+        print(f"PAVRM toy step {s}: median distance to the fp32 truth ours {med(ours):.4e}, "
+              f"reference {med(refs):.4e}, ratio {med(ours) / med(refs):.4f}")
+        assert med(ours) <= 1.01 * med(refs), (s, med(ours), med(refs), worst)
         if s == 0:
             # same weights and inputs as the reference: every tensor within 1.5x its worst error
             assert max(ours.values()) <= 1.5 * max(refs.values()), (s, worst, max(refs.values()))
