@@ -824,7 +824,8 @@ constexpr int A64SLOT = 32768;
 // different MFMA gap of the chunk -- after MFMA {0, 3, 5, 7}[wave] or 2 x wave -- so the four
 // waves' pieces do not reach the texture-address unit together: 0.5-2.5 % slower.  A build without
 // the DMA runs 14 % faster and one without its vmcnt waits no faster (profiles/r05_ab_gemm_diag.txt):
-// what the pieces cost is neither the data's arrival nor the four waves' collision.)
+// what the pieces cost is neither the data's arrival nor the four waves' collision.  Moving every
+// wave's piece to MFMA gap 3, 5 or 7 of the chunk ties within 0.5 %, profiles/r05_ab_gemm_dgap.txt.)
 #ifndef GEMM4_DIAG
 #define GEMM4_DIAG 0
 #endif
