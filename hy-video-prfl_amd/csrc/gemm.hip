@@ -825,7 +825,11 @@ constexpr int A64SLOT = 32768;
 // waves' pieces do not reach the texture-address unit together: 0.5-2.5 % slower.  A build without
 // the DMA runs 14 % faster and one without its vmcnt waits no faster (profiles/r05_ab_gemm_diag.txt):
 // what the pieces cost is neither the data's arrival nor the four waves' collision.  Moving every
-// wave's piece to MFMA gap 3, 5 or 7 of the chunk ties within 0.5 %, profiles/r05_ab_gemm_dgap.txt.)
+// wave's piece to MFMA gap 3, 5 or 7 of the chunk ties within 0.5 %, profiles/r05_ab_gemm_dgap.txt.
+// Also measured and dropped: the TN forward with B staged 64 deep too (hipBLASLt's operand format,
+// one ds_read_b128 per B fragment; A's three 64-deep slots + B's two fill the 160 KiB, so a B slice
+// has one step to land instead of two): bit-identical, 4-8 % SLOWER than the 32-deep forms,
+// profiles/r05_ab_gemm_b64.txt.)
 #ifndef GEMM4_DIAG
 #define GEMM4_DIAG 0
 #endif
