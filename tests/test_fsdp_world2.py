@@ -154,6 +154,27 @@ def _run(rank, wrap_fused, out_q):
     dist.barrier()
 
 
+def _ref_worker(out_q):
+    torch.set_num_threads(4)
+    _register_cpu_standins()
+    from prfl_amd.model import WanModel
+    from shapes import TOY, model_shapes, seeded_params
+    ref = WanModel(model_type="t2v", in_dim=16, **TOY)
+    ref.load_state_dict(seeded_params(model_shapes(TOY, "t2v"), prefix="toy."))
+    t = torch.tensor([700])
+    outs = []
+    for r in range(2):
+        x, c, up = _sample(r)
+        out = ref(x=[x], t=t, context=[c], seq_len=105)[0]
+        outs.append(out.detach().numpy())
+        ((out * up).sum() / 2).backward()
+    gn = torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm=1e9)
+    grads = {n: p.grad.detach().clone().numpy() for n, p in ref.named_parameters()
+             if p.grad is not None}
+    torch.optim.SGD(ref.parameters(), lr=1.0).step()
+    out_q.put((outs, float(gn), {n: p.detach().numpy() for n, p in ref.named_parameters()}, grads))
+
+
 @pytest.mark.parametrize("wrap_fused", [False, True])
 def test_fsdp_full_shard_world2_composes_with_fused_block(wrap_fused):
     ctx = mp.get_context("spawn")
@@ -171,35 +192,31 @@ def test_fsdp_full_shard_world2_composes_with_fused_block(wrap_fused):
     # FULL_SHARD really sharded: each rank holds about half of the parameters
     for _, _, _, _, n_local, n_total in res:
         assert n_local < 0.6 * n_total
-    # the reference: the same model unwrapped, both samples in one process, loss halved per sample
-    _register_cpu_standins()
-    from prfl_amd.model import WanModel
-    from shapes import TOY, model_shapes, seeded_params
-    torch.set_num_threads(4)
-    ref = WanModel(model_type="t2v", in_dim=16, **TOY)
-    ref.load_state_dict(seeded_params(model_shapes(TOY, "t2v"), prefix="toy."))
-    t = torch.tensor([700])
+    # the reference: the same model unwrapped, both samples in one (spawned: the CPU stand-ins
+    # must not stay registered in this process) process, loss halved per sample
+    rq = ctx.Queue()
+    rp = ctx.Process(target=_ref_worker, args=(rq,))
+    rp.start()
+    ref_outs, gn_ref, ref_params, ref_grads = rq.get(timeout=300)
+    rp.join(timeout=60)
+    assert rp.exitcode == 0
     for r in range(2):
-        x, c, up = _sample(r)
-        out = ref(x=[x], t=t, context=[c], seq_len=105)[0]
-        assert torch.equal(torch.from_numpy(res[r][1]), out.detach()), f"rank {r} forward"
-        ((out * up).sum() / 2).backward()
-    gn_ref = torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm=1e9)
-    assert abs(res[0][2] / gn_ref.item() - 1) < 1e-5 and res[0][2] == res[1][2]
-    torch.optim.SGD(ref.parameters(), lr=1.0).step()
+        assert torch.equal(torch.from_numpy(res[r][1]), torch.from_numpy(ref_outs[r])), f"rank {r} forward"
+    assert abs(res[0][2] / gn_ref - 1) < 1e-5 and res[0][2] == res[1][2]
     # FSDP's reduce (each rank's gradient pre-divided by 2, then summed: exact) and the reference's
     # accumulation agree up to the order in which autograd sums a parameter's uses (the time
     # embedding feeds every block): held to 1e-5 of the gradient's scale plus the fp32 rounding of
     # p - g
     n_cmp, worst = 0, 0.0
-    for n, p in ref.named_parameters():
-        if p.grad is None:
+    for n, pv in ref_params.items():
+        if n not in ref_grads:
             continue
+        p, g = torch.from_numpy(pv), torch.from_numpy(ref_grads[n])
         a = torch.from_numpy(res[0][3][n])
         assert torch.equal(a, torch.from_numpy(res[1][3][n])), n        # replicas agree
-        err = (a - p.detach()).abs().max().item()
-        scale = p.grad.abs().max().item()
-        assert err <= 1e-5 * scale + 2e-6 * max(1.0, p.detach().abs().max().item()), (n, err, scale)
+        err = (a - p).abs().max().item()
+        scale = g.abs().max().item()
+        assert err <= 1e-5 * scale + 2e-6 * max(1.0, p.abs().max().item()), (n, err, scale)
         worst = max(worst, err / max(scale, 1e-30))
         n_cmp += 1
     assert n_cmp > 30
