@@ -125,8 +125,8 @@ __device__ __forceinline__ int rope_index(int pair, int pf, int ph, int pw) {
 
 __global__ __launch_bounds__(NT) void rms_rope_fwd_kernel(
     const bf16* __restrict__ x, int64_t ldx, int C, const float* __restrict__ w, float eps,
-    const float2* __restrict__ tab, int F, int Hg, int Wg, bf16* __restrict__ out, int64_t ldo,
-    float* __restrict__ rstd_out, float oscale) {
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ out,
+    int64_t ldo, float* __restrict__ rstd_out, float oscale) {
   __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
   const int nc = C / 4;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(NT) void rms_rope_fwd_kernel(
   const float rstd = rsqrtf(block_sum<NT>(ss, red) / C + eps);
   int pf, ph, pw;
   bool rot;
-  rope_pos(row, F, Hg, Wg, pf, ph, pw, rot);
+  rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
   rot = rot && tab != nullptr;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
@@ -180,8 +180,8 @@ template <int ROWS>
 __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
     const bf16* __restrict__ dout, int64_t lddo, const bf16* __restrict__ x, int64_t ldx,
     const float* __restrict__ rstd_in, int L, int C, const float* __restrict__ w,
-    const float2* __restrict__ tab, int F, int Hg, int Wg, bf16* __restrict__ dx, int64_t lddx,
-    float* __restrict__ part0, float oscale) {
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ dx,
+    int64_t lddx, float* __restrict__ part0, float oscale) {
   __shared__ float red[NT / 64];
   const int nc = C / 4;
   f32x4 p0[MAXV];
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
     const float rstd = rstd_in[row];
     int pf, ph, pw;
     bool rot;
-    rope_pos(row, F, Hg, Wg, pf, ph, pw, rot);
+    rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
     rot = rot && tab != nullptr;
     float s = 0.f;
     // pass 1: s = sum(dn * xhat); pass 2 recomputes dn from the re-read row
@@ -362,23 +362,51 @@ extern "C" int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int 
   return 0;
 }
 
-extern "C" int prfl_rms_rope_fwd_scaled(const void* x, int64_t ldx, int64_t L, int64_t C,
-                                        const float* w, float eps, const float* rope_tab,
-                                        int64_t F, int64_t Hg, int64_t Wg, void* out, int64_t ldo,
-                                        float* rstd, float out_scale, void* stream) {
+extern "C" int prfl_rms_rope_fwd_pos(const void* x, int64_t ldx, int64_t L, int64_t C,
+                                     const float* w, float eps, const float* rope_tab, int64_t F,
+                                     int64_t Hg, int64_t Wg, int64_t row0, void* out, int64_t ldo,
+                                     float* rstd, float out_scale, void* stream) {
   if (L <= 0) return 0;
-  if (bad_c(C)) return (int)hipErrorInvalidValue;
+  if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
   // (a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p:
   // profiles/r03_ab_rms_rope_wave.txt)
   hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C, w,
-                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)out, ldo, rstd,
-                     out_scale);
+                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)out, ldo,
+                     rstd, out_scale);
   prfl_prof::set_work((double)L * C * 4);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int prfl_rms_rope_bwd_pos(const void* dout, int64_t lddo, const void* x, int64_t ldx,
+                                     const float* rstd, int64_t L, int64_t C, const float* w,
+                                     const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg,
+                                     int64_t row0, void* dx, int64_t lddx, float* part0,
+                                     float out_scale, void* stream) {
+  if (L <= 0) return 0;
+  if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  prfl_prof::begin(KID_RMS, s);
+  hipLaunchKernelGGL(rms_rope_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
+                     0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L, (int)C, w,
+                     (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)dx, lddx,
+                     part0, out_scale);
+  prfl_prof::set_work((double)L * C * 6);
+  prfl_prof::end(KID_RMS, s);
+  PRFL_LAUNCH_CHECK();
+  return 0;
+}
+
+// the round-3 entries: positions counted from row 0
+extern "C" int prfl_rms_rope_fwd_scaled(const void* x, int64_t ldx, int64_t L, int64_t C,
+                                        const float* w, float eps, const float* rope_tab,
+                                        int64_t F, int64_t Hg, int64_t Wg, void* out, int64_t ldo,
+                                        float* rstd, float out_scale, void* stream) {
+  return prfl_rms_rope_fwd_pos(x, ldx, L, C, w, eps, rope_tab, F, Hg, Wg, 0, out, ldo, rstd,
+                               out_scale, stream);
 }
 
 extern "C" int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const void* x,
@@ -386,17 +414,6 @@ extern "C" int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const vo
                                         const float* w, const float* rope_tab, int64_t F,
                                         int64_t Hg, int64_t Wg, void* dx, int64_t lddx,
                                         float* part0, float out_scale, void* stream) {
-  if (L <= 0) return 0;
-  if (bad_c(C)) return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
-  prfl_prof::begin(KID_RMS, s);
-  hipLaunchKernelGGL(rms_rope_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
-                     0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L, (int)C, w,
-                     (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, (bf16*)dx, lddx, part0,
-                     out_scale);
-  prfl_prof::set_work((double)L * C * 6);
-  prfl_prof::end(KID_RMS, s);
-  PRFL_LAUNCH_CHECK();
-  return 0;
+  return prfl_rms_rope_bwd_pos(dout, lddo, x, ldx, rstd, L, C, w, rope_tab, F, Hg, Wg, 0, dx, lddx,
+                               part0, out_scale, stream);
 }
-

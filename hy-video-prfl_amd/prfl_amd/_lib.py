@@ -55,6 +55,9 @@ SIGNATURES = {
     "prfl_rms_rope_fwd_scaled": [P, I64, I64, I64, P, F32, P, I64, I64, I64, P, I64, P, F32, P],
     "prfl_rms_rope_bwd_scaled": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, P, I64, P, F32,
                                  P],
+    "prfl_rms_rope_fwd_pos": [P, I64, I64, I64, P, F32, P, I64, I64, I64, I64, P, I64, P, F32, P],
+    "prfl_rms_rope_bwd_pos": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, I64, P, I64, P, F32,
+                              P],
     "prfl_cast_f32_bf16": [P, P, I64, P],
     "prfl_cast_f32_bf16_t": [P, I64, I64, I64, P, I64, P],
     "prfl_gate_bwd": [P, I64, P, I64, P, I64, I64, P, I64, P, P, P],

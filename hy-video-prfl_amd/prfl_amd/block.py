@@ -15,6 +15,7 @@ normalised q/k, residual stream fp32.
 import torch
 
 from . import ops
+from . import sp as SP
 from .ops import BF16, EPI_BF16, EPI_GELU, EPI_RESID, EPI_DGELU
 
 T5_CONTEXT_TOKEN_NUMBER = 512  # model.py:18
@@ -68,8 +69,11 @@ def credit_attn_stash(nbytes):
 class Meta:
     """Non-tensor block arguments."""
 
-    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6, fp8=0):
+    def __init__(self, num_heads, grid, seq_len, rope_tab, i2v, eps=1e-6, fp8=0, sp=None):
         self.num_heads = num_heads
+        # Ulysses sequence parallelism (sp.SPState or None): x holds this rank's L tokens, the
+        # rank's tokens start at position sp.rank * L of the padded sequence (sp.py)
+        self.sp = sp
         # config C5 (WanModel.set_fp8_gemm): 0 bf16; 1 e4m3 forward projections; 2 also the e4m3
         # self-attention forward (ops.attn_fwd_fp8; its backward stays bf16 on that forward's O/LSE)
         self.fp8 = int(fp8)
@@ -183,16 +187,37 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False
     grid = meta.grid[b]
     # q leaves RMSNorm+RoPE already in log2 units (x softmax_scale * log2 e, one bf16 rounding as
     # before): the attention kernels then take one v_exp per score (ops.L2Q_SCALE, q_log2)
+    st = meta.sp
+    row0 = st.rank * L if st is not None else 0     # the rank's first token (model.py:89-96)
     qr, rq = ops.rms_rope_fwd(q_raw, g("self_attn.norm_q.weight"), eps, meta.rope_tab, grid,
-                              out_scale=ops.L2Q_SCALE)
-    kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid)
-    if attn is not None:
-        ao, lse = attn
+                              out_scale=ops.L2Q_SCALE, row0=row0)
+    kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid,
+                              row0=row0)
+    fwd = ops.attn_fwd_fp8 if meta.fp8 >= 2 else ops.attn_fwd
+    if st is None:
+        if attn is not None:
+            ao, lse = attn
+        else:
+            ao, lse = fwd(qr, kr, v, nh, k_len=meta.seq_len[b], q_log2=True)
+        if keep_attn:
+            S["attn"] = (ao, lse)
     else:
-        fwd = ops.attn_fwd_fp8 if meta.fp8 >= 2 else ops.attn_fwd
-        ao, lse = fwd(qr, kr, v, nh, k_len=meta.seq_len[b], q_log2=True)
-    if keep_attn:
-        S["attn"] = (ao, lse)
+        # Ulysses: all tokens of this rank's nh / P heads (model.py:183-196); the kept output
+        # is the head-sharded one, viewed in the [L, C] / [H, L] shapes of the unsharded stash
+        P, Sq = st.size, st.size * L
+        full = None
+        if attn is None or save:
+            full = SP.qkv_to_heads(qr, kr, v, st)
+        if attn is not None:
+            ao_full, lse = attn[0].view(Sq, C // P), attn[1].view(nh // P, Sq)
+        else:
+            ao_full, lse = fwd(full[1], full[2], full[3], nh // P, k_len=meta.seq_len[b],
+                               q_log2=True)
+        if keep_attn:
+            S["attn"] = (ao_full.view(L, C), lse.view(nh, L))
+        ao = SP.heads_to_seq(ao_full, st)
+        if save:
+            S.update(qkv_full=full[0], ao_full=ao_full)
     y1 = torch.empty(L, C, dtype=BF16, device=x.device) if save else None
     x1 = lin(W, "o", ao, epilogue=EPI_RESID, gate=e[2], res=x, aux=y1)
     if save:
@@ -333,13 +358,33 @@ def block_backward_one(P, W, x, e, ctx, meta, b, S, dout, G, want_w=True):
     del dy1
     qkv = S["qkv"]
     dqkv = torch.empty(L, 3 * C, dtype=BF16, device=x.device)
-    dqr, dkr, _ = ops.attn_bwd(S["qr"], S["kr"], qkv[:, 2 * C:], S["ao"], dao, S["lse"], nh,
-                               k_len=meta.seq_len[b], dv=dqkv[:, 2 * C:], q_log2=True)
+    st = meta.sp
+    if st is None:
+        row0 = 0
+        dqr, dkr, _ = ops.attn_bwd(S["qr"], S["kr"], qkv[:, 2 * C:], S["ao"], dao, S["lse"], nh,
+                                   k_len=meta.seq_len[b], dv=dqkv[:, 2 * C:], q_log2=True)
+    else:
+        # the inverse exchange: d(out) to this rank's heads, the attention backward over all
+        # tokens into one [S, 3, C/P] dq | dk | dv image, back to this rank's tokens
+        row0 = st.rank * L
+        P = st.size
+        dao_full = SP.seq_to_heads(dao, st)
+        full = S["qkv_full"]
+        dfull = torch.empty_like(full)
+        ops.attn_bwd(full[:, 0], full[:, 1], full[:, 2], S["ao_full"], dao_full, S["lse"], nh // P,
+                     k_len=meta.seq_len[b], dq=dfull[:, 0], dk=dfull[:, 1], dv=dfull[:, 2],
+                     q_log2=True)
+        del dao_full
+        dqr = torch.empty(L, C, dtype=BF16, device=x.device)
+        dkr = torch.empty(L, C, dtype=BF16, device=x.device)
+        SP.dqkv_to_seq(dfull, st, dqr, dkr, dqkv[:, 2 * C:])
+        del dfull
     del dao
     _, dnq = ops.rms_rope_bwd(dqr, qkv[:, :C], S["rq"], g("self_attn.norm_q.weight"),
-                              meta.rope_tab, grid, dx=dqkv[:, :C], out_scale=ops.L2Q_SCALE)
+                              meta.rope_tab, grid, dx=dqkv[:, :C], out_scale=ops.L2Q_SCALE,
+                              row0=row0)
     _, dnk = ops.rms_rope_bwd(dkr, qkv[:, C:2 * C], S["rk"], g("self_attn.norm_k.weight"),
-                              meta.rope_tab, grid, dx=dqkv[:, C:2 * C])
+                              meta.rope_tab, grid, dx=dqkv[:, C:2 * C], row0=row0)
     acc("self_attn.norm_q.weight", dnq)
     acc("self_attn.norm_k.weight", dnk)
     del dqr, dkr
@@ -376,5 +421,5 @@ def block_apply(P, x, e, context, meta, allow_keep=True):
     grid = [int(v) for g in meta.grid for v in g]
     out, _, _ = custom_ops.wan_block(x, e, context, params, int(meta.num_heads), grid,
                                      [int(v) for v in meta.seq_len], meta.rope_tab, bool(meta.i2v),
-                                     float(meta.eps), int(meta.fp8), keep)
+                                     float(meta.eps), int(meta.fp8), keep, SP.register(meta.sp))
     return out

@@ -26,6 +26,7 @@ from torch import Tensor
 
 from . import block as B
 from . import ops
+from . import sp as SP
 from .ops import BF16
 
 F32 = torch.float32
@@ -36,21 +37,23 @@ def _empty(like, dtype=None):
 
 
 # ============================================================ fused WanAttentionBlock ======
-def _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8):
+def _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp=0):
     g = [tuple(grid[i:i + 3]) for i in range(0, len(grid), 3)]
-    return B.Meta(num_heads, g, list(seq_lens), rope_tab, i2v, eps, fp8=fp8)
+    return B.Meta(num_heads, g, list(seq_lens), rope_tab, i2v, eps, fp8=fp8, sp=SP.lookup(sp))
 
 
 @torch.library.custom_op("prfl::wan_block", mutates_args=(), device_types="cuda")
 def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_heads: int,
               grid: List[int], seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float,
-              fp8: int, keep_attn: bool) -> Tuple[Tensor, Tensor, Tensor]:
+              fp8: int, keep_attn: bool, sp: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
     """fp8: 0 bf16, 1 e4m3 forward projections, 2 also the e4m3 self-attention forward
     (config C5, block.Meta).  x [B, L, C] (fp32, or bf16 for block 0), e [B, 6, C] fp32 (modulation + e0), context
     [B, Lc, C] bf16, params in block.param_names(i2v) order, grid = flattened (F, H, W) per
     sample.  Returns (out fp32 [B, L, C], kept self-attention output bf16 [B, L, C] and LSE fp32
-    [B, H, L] when keep_attn, else empty)."""
-    meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8)
+    [B, H, L] when keep_attn, else empty).  sp: a sequence-parallel group handle (prfl_amd.sp;
+    0 = none): x then holds this rank's tokens and the self-attention runs Ulysses-sharded, the
+    kept output / LSE being the head-sharded ones in the same shapes."""
+    meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp)
     P = dict(zip(B.param_names(i2v), params))
     W = B.BF16Weights(P, fp8=fp8 > 0, need_bf16=False)
     outs, aos, lses = [], [], []
@@ -71,7 +74,7 @@ def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_h
 
 
 @wan_block.register_fake
-def _(x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, keep_attn):
+def _(x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, keep_attn, sp=0):
     Bn, L, C = x.shape
     out = x.new_empty((Bn, L, C), dtype=F32)
     if keep_attn:
@@ -83,11 +86,11 @@ def _(x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8,
 def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, params: List[Tensor],
                        ao: Tensor, lse: Tensor, num_heads: int, grid: List[int],
                        seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float, fp8: int,
-                       want_w: bool, want_ctx: bool) -> List[Tensor]:
+                       want_w: bool, want_ctx: bool, sp: int = 0) -> List[Tensor]:
     """Recompute the block forward (reusing a kept (ao, lse) when given), then the backward
     chain.  Returns [dx (x.dtype), de fp32, dctx (context.dtype or empty), *dparams (param
     dtype, or empty when not want_w)]."""
-    meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8)
+    meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp)
     names = B.param_names(i2v)
     P = dict(zip(names, params))
     W = B.BF16Weights(P, fp8=fp8 > 0)
@@ -113,36 +116,37 @@ def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, para
 
 @wan_block_backward.register_fake
 def _(dout, x, e, context, params, ao, lse, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8,
-      want_w, want_ctx):
+      want_w, want_ctx, sp=0):
     res = [torch.empty_like(x), e.new_empty(e.shape, dtype=F32),
            torch.empty_like(context) if want_ctx else _empty(context)]
     return res + [torch.empty_like(p) if want_w else _empty(p) for p in params]
 
 
 def _wan_block_setup(ctx, inputs, output):
-    x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, keep = inputs
+    x, e, context, params, num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, keep, sp = inputs
     _, ao, lse = output
     ctx.mark_non_differentiable(ao, lse)
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(x, e, context, rope_tab, ao, lse, *params)
-    ctx.args = (num_heads, list(grid), list(seq_lens), i2v, eps, fp8)
+    ctx.args = (num_heads, list(grid), list(seq_lens), i2v, eps, fp8, sp)
     ctx.req = (x.requires_grad, e.requires_grad, context.requires_grad,
                [p.requires_grad for p in params])
 
 
 def _wan_block_bwd(ctx, dout, _dao, _dlse):
     x, e, context, rope_tab, ao, lse, *params = ctx.saved_tensors
-    nh, grid, seq_lens, i2v, eps, fp8 = ctx.args
+    nh, grid, seq_lens, i2v, eps, fp8, sp = ctx.args
     rx, re, rc, rp = ctx.req
     if ao.numel():                      # the kept (ao, lse) die with this node (block.py)
         B.credit_attn_stash(B.stash_bytes(ao, lse))
+    # one entry per argument the caller passed (a trailing `sp` left at its default is not one)
+    tail = (None,) * (len(ctx.needs_input_grad) - 4)
     if dout is None:
-        return (None,) * 3 + ([None] * len(params),) + (None,) * 8
+        return (None,) * 3 + ([None] * len(params),) + tail
     res = wan_block_backward(dout.contiguous(), x, e, context, params, ao, lse, nh, grid,
-                             seq_lens, rope_tab, i2v, eps, fp8, any(rp), rc)
+                             seq_lens, rope_tab, i2v, eps, fp8, any(rp), rc, sp)
     dps = [d if r else None for d, r in zip(res[3:], rp)]
-    return (res[0] if rx else None, res[1] if re else None, res[2] if rc else None, dps,
-            None, None, None, None, None, None, None, None)
+    return (res[0] if rx else None, res[1] if re else None, res[2] if rc else None, dps) + tail
 
 
 wan_block.register_autograd(_wan_block_bwd, setup_context=_wan_block_setup)

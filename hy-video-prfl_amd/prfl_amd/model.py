@@ -15,7 +15,6 @@ What runs where:
 import json
 import math
 import os
-import sys
 
 import torch
 import torch.nn as nn
@@ -23,6 +22,7 @@ import torch.nn.functional as F
 
 from . import block as B
 from . import ops
+from . import sp as SP
 from .linear import linear_bf16
 
 __all__ = ["WanModel", "WanAttentionBlock", "WanRMSNorm", "WanLayerNorm", "rope_params",
@@ -58,24 +58,32 @@ def pad_freqs(original_tensor, target_len):
 
 
 def rope_apply(x, grid_sizes, freqs):
-    """model.py:61-103 on the HIP kernel path is fused into RMSNorm (prfl_rms_rope_fwd); this
-    standalone form (fp64, as the reference) is kept for API compatibility."""
+    """model.py:61-103.  On the HIP path RoPE is fused into RMSNorm (prfl_rms_rope_fwd_pos);
+    this standalone form (fp64, as the reference) serves the attention sub-modules.  Under
+    sequence parallelism x holds this rank's s tokens, rotated by their positions
+    [rank * s, (rank + 1) * s) in the whole sequence, unit multipliers past the grid
+    (model.py:89-96)."""
     b, s, n, d = x.shape
     c = d // 2
+    st = SP.current()
+    row0 = st.rank * s if st is not None else 0
     fs = freqs.to(x.device).split([c - 2 * (c // 3), c // 3, c // 3], dim=1)
     out = []
     for i, (f, h, w) in enumerate(grid_sizes.tolist()):
         L = f * h * w
-        xi = torch.view_as_complex(x[i, :L].to(torch.float64).reshape(L, n, -1, 2))
         fi = torch.cat([fs[0][:f].view(f, 1, 1, -1).expand(f, h, w, -1),
                         fs[1][:h].view(1, h, 1, -1).expand(f, h, w, -1),
                         fs[2][:w].view(1, 1, w, -1).expand(f, h, w, -1)], dim=-1).reshape(L, 1, -1)
-        out.append(torch.cat([torch.view_as_real(xi * fi).flatten(2), x[i, L:].to(torch.float64)]))
+        fi = pad_freqs(fi, row0 + s)[row0:row0 + s]           # rows past the grid: unit
+        n_rot = max(0, min(s, L - row0))
+        xi = torch.view_as_complex(x[i, :n_rot].to(torch.float64).reshape(n_rot, n, -1, 2))
+        out.append(torch.cat([torch.view_as_real(xi * fi[:n_rot]).flatten(2),
+                              x[i, n_rot:].to(torch.float64)]))
     return torch.stack(out).float()
 
 
 class WanRMSNorm(nn.Module):
-    """model.py:106-122.  Inside a block the kernel prfl_rms_rope_fwd computes it; standalone
+    """model.py:106-122.  Inside a block the kernel prfl_rms_rope_fwd_pos computes it; standalone
     calls use the same fp32 formula."""
 
     def __init__(self, dim, eps=1e-5):
@@ -134,11 +142,17 @@ class _Attn(nn.Module):
 
 class WanSelfAttention(_Attn):
     def forward(self, x, seq_lens, grid_sizes, freqs):
-        """model.py:163-201 (no sequence parallelism: DP replaces SP)."""
+        """model.py:163-201; under sequence parallelism q/k/v go to (all tokens, this rank's
+        heads) and the output back, each exchange with its inverse as backward (sp.py)."""
         from .attention import flash_attention
         q, k, v = self._qkv(x, x)
         q, k = rope_apply(q, grid_sizes, freqs), rope_apply(k, grid_sizes, freqs)
+        st = SP.current()
+        if st is not None:
+            q, k, v = (SP.all_to_all_4d(t, st, True) for t in (q, k, v))
         a = flash_attention(q, k, v, k_lens=seq_lens, window_size=self.window_size)
+        if st is not None:
+            a = SP.all_to_all_4d(a, st, False)
         return self._proj("o", a.flatten(2))
 
 
@@ -223,9 +237,13 @@ class WanAttentionBlock(nn.Module):
         with torch.autocast("cuda", enabled=False):
             em = self.modulation + e                                   # model.py:340
             P = {n: self._param(n) for n in self._names}
+            st = SP.current()
+            if st is not None and self.num_heads % st.size:
+                raise ValueError(f"sequence parallelism: {self.num_heads} heads do not split over "
+                                 f"sp_size {st.size}")
             meta = B.Meta(self.num_heads, [tuple(g) for g in grid_sizes.tolist()],
                           [int(s) for s in seq_lens.tolist()], _rope_table(freqs, x.device),
-                          self.i2v, self.eps, fp8=self.fp8_gemm)
+                          self.i2v, self.eps, fp8=self.fp8_gemm, sp=st)
             ctx = context if context.dtype == torch.bfloat16 else context.to(torch.bfloat16)
             return B.block_apply(P, x.contiguous(), em.contiguous(), ctx.contiguous(), meta,
                                  allow_keep=self.stash_attn)
@@ -270,25 +288,6 @@ class MLPProj(nn.Module):
             h = F.gelu(h)                                            # bf16 in, bf16 out
             h = linear_bf16(h, p[3].weight, p[3].bias)
             return F.layer_norm(h.float(), p[4].normalized_shape, p[4].weight, p[4].bias, p[4].eps)
-
-
-def _refuse_sequence_parallel():
-    """The reference chunks the token sequence across an initialised Ulysses group
-    (`model.py:618-619`, all-to-all `:183-196`, all-gather `:663-676`); this package runs pure
-    data parallelism.  Every shipped training config sets `sp_size: 4`
-    (`configs/train_prfl_t2v_720.yaml:51`): run under it, each rank of a 4-rank group would get
-    the same sample from the sampler (`train_prfl.py:455-464`) and compute the full sequence —
-    4x redundant work with no error.  So an initialised SP state (read from the reference's own
-    `diffusers_lite.utils.parallel_states` if the driver imported it; nothing is imported here)
-    is refused loudly."""
-    ps = sys.modules.get("diffusers_lite.utils.parallel_states")
-    get = getattr(ps, "get_sequence_parallel_state", None)
-    if callable(get) and get():
-        sp = getattr(getattr(ps, "nccl_info", None), "sp_size", "> 1")
-        raise RuntimeError(
-            f"sequence parallelism is initialised (sp_size {sp}), but this WanModel runs pure data "
-            "parallelism: set `sp_size: 1` in the training YAML (INTEGRATION.md, 'Configs').  "
-            "Running on would make every rank of an SP group compute the same sample in full.")
 
 
 class WanModel(nn.Module):
@@ -430,18 +429,27 @@ class WanModel(nn.Module):
 
     def forward(self, x, t, context, seq_len, clip_fea=None, y=None, cond_flag=False,
                 output_features=False, selected_layers=[20, 30, 40]):
-        _refuse_sequence_parallel()
+        """model.py:534-681.  Under the reference's sequence parallelism (its `parallel_states`
+        initialised with sp_size > 1, or `prfl_amd.sp.set_group`) each rank runs the blocks on
+        its seq_len / sp_size tokens (model.py:618-619) and the features / head output are
+        all-gathered along the sequence (model.py:663-676), exactly as the reference."""
         xb, e, e0, ctx, grid_sizes, seq_lens, grids = self._embed(x, t, context, seq_len,
                                                                  clip_fea, y)
-        feats = []
+        st = SP.current()
         h = xb
+        if st is not None:
+            s = SP.split_len(xb.shape[1], st)
+            h = xb.narrow(1, st.rank * s, s)                 # torch.chunk(x, sp, 1)[rank]
+        feats = []
         for index, block in enumerate(self.blocks):
             h = block(h, e0, seq_lens, grid_sizes, self.freqs, ctx, None)
             if output_features and index + 1 in selected_layers:
-                feats.append(h)
+                feats.append(SP.gather_seq(h, st) if st is not None else h)
         if output_features:
             return feats
         out = self.head(h, e)
+        if st is not None:
+            out = SP.gather_seq(out, st)
         return [u.float() for u in self.unpatchify(out, grid_sizes, self.out_dim)]
 
     def unpatchify(self, x, grid_sizes, c):

@@ -220,28 +220,31 @@ def ln_mod_bwd(dy, x, mean, rstd, dx, scale=None, w=None, accumulate=True):
 L2Q_SCALE = 1.4426950408889634 / math.sqrt(128)
 
 
-def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None, out_scale=1.0):
+def rms_rope_fwd(x, w, eps=1e-6, rope_tab=None, grid=(0, 0, 0), out=None, out_scale=1.0, row0=0):
+    """bf16(rope(bf16(x * rsqrt(mean x^2 + eps)) * w) * out_scale); row r is token row0 + r of
+    the grid (row0 > 0: a sequence-parallel rank's shard, model.py:89-96)."""
     L, C = x.shape
     if out is None:
         out = torch.empty(L, C, dtype=BF16, device=x.device)
     rstd = torch.empty(L, dtype=torch.float32, device=x.device)
     f, h, ww = grid
-    call("prfl_rms_rope_fwd_scaled", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps), ptr(rope_tab),
-         I64(f), I64(h), I64(ww), ptr(out), I64(_ld(out)), ptr(rstd), F32(out_scale), stream_ptr())
+    call("prfl_rms_rope_fwd_pos", ptr(x), I64(_ld(x)), I64(L), I64(C), ptr(w), F32(eps),
+         ptr(rope_tab), I64(f), I64(h), I64(ww), I64(row0), ptr(out), I64(_ld(out)), ptr(rstd),
+         F32(out_scale), stream_ptr())
     return out, rstd
 
 
-def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_scale=1.0):
-    """returns (dx bf16, d w fp32); out_scale as the forward's (dout is scaled by it)."""
+def rms_rope_bwd(dout, x, rstd, w, rope_tab=None, grid=(0, 0, 0), dx=None, out_scale=1.0, row0=0):
+    """returns (dx bf16, d w fp32); out_scale and row0 as the forward's (dout is scaled by it)."""
     L, C = x.shape
     rp = call_int("prfl_norm_rows_per_part")
     p0 = torch.empty((L + rp - 1) // rp, C, dtype=torch.float32, device=x.device)
     if dx is None:
         dx = torch.empty(L, C, dtype=BF16, device=x.device)
     f, h, ww = grid
-    call("prfl_rms_rope_bwd_scaled", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd), I64(L),
-         I64(C), ptr(w), ptr(rope_tab), I64(f), I64(h), I64(ww), ptr(dx), I64(_ld(dx)), ptr(p0),
-         F32(out_scale), stream_ptr())
+    call("prfl_rms_rope_bwd_pos", ptr(dout), I64(_ld(dout)), ptr(x), I64(_ld(x)), ptr(rstd),
+         I64(L), I64(C), ptr(w), ptr(rope_tab), I64(f), I64(h), I64(ww), I64(row0), ptr(dx),
+         I64(_ld(dx)), ptr(p0), F32(out_scale), stream_ptr())
     return dx, colsum_reduce(p0)
 
 

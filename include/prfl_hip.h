@@ -213,6 +213,19 @@ int prfl_rms_rope_bwd_scaled(const void* dout, int64_t lddo, const void* x, int6
                              const float* rstd, int64_t L, int64_t C, const float* w,
                              const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, void* dx,
                              int64_t lddx, float* part0, float out_scale, void* stream);
+/* The same two with the rows' sequence positions starting at row0 instead of 0: row r of x is
+ * token row0 + r of the (F,Hg,Wg) grid, positions >= F*Hg*Wg pass unrotated.  This is the
+ * sequence-parallel rope_apply of model.py:89-96 (a rank of an SP group holds tokens
+ * [rank * s, (rank + 1) * s) of the padded sequence and rotates them by those positions'
+ * frequencies, pad_freqs' unit multipliers past the grid).  The _scaled entries are row0 = 0. */
+int prfl_rms_rope_fwd_pos(const void* x, int64_t ldx, int64_t L, int64_t C, const float* w,
+                          float eps, const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg,
+                          int64_t row0, void* out, int64_t ldo, float* rstd, float out_scale,
+                          void* stream);
+int prfl_rms_rope_bwd_pos(const void* dout, int64_t lddo, const void* x, int64_t ldx,
+                          const float* rstd, int64_t L, int64_t C, const float* w,
+                          const float* rope_tab, int64_t F, int64_t Hg, int64_t Wg, int64_t row0,
+                          void* dx, int64_t lddx, float* part0, float out_scale, void* stream);
 
 /* ---- element-wise / reductions ------------------------------------------------------------ */
 /* autocast weight cast fp32 -> bf16 (the .to(bf16) of every Linear weight under autocast). */

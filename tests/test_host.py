@@ -318,24 +318,32 @@ def test_loss_guard_matches_reference_semantics():
 
 
 @pytest.mark.parametrize("state", [True, False])
-def test_forward_refuses_initialised_sequence_parallel(monkeypatch, state):
-    """with the reference's `parallel_states` reporting an initialised SP group
-    (as every shipped YAML's `sp_size: 4` leaves it), WanModel.forward raises and names the fix,
-    instead of running 4x redundant work; with SP off it proceeds (to the HIP op, which has no
-    CPU path here)."""
+def test_sp_state_follows_reference_parallel_states(monkeypatch, state):
+    """The drop-in reads the reference's own `parallel_states` (initialised by the drivers from
+    the YAML's `sp_size`, `train_prfl.py:118`): with SP on, `prfl_amd.sp.current()` reports the
+    group, rank and size of `nccl_info` and WanModel.forward runs the Ulysses path (round 5
+    refused it instead); an explicit `sp.set_group(False)` overrides it."""
     import sys
     import types
-    from prfl_amd.model import WanModel
+    from prfl_amd import sp
     ps = types.ModuleType("diffusers_lite.utils.parallel_states")
     ps.get_sequence_parallel_state = lambda: state
-    ps.nccl_info = types.SimpleNamespace(sp_size=4 if state else 1)
+    grp = object()
+    ps.nccl_info = types.SimpleNamespace(sp_size=4 if state else 1, group=grp,
+                                         rank_within_group=2 if state else 0)
     monkeypatch.setitem(sys.modules, "diffusers_lite.utils.parallel_states", ps)
-    m = WanModel(dim=64, ffn_dim=128, num_heads=2, num_layers=1, in_dim=16)
-    x = [torch.randn(16, 1, 4, 4)]
-    ctx = [torch.randn(8, 4096)]
+    sp.clear()
+    st = sp.current()
     if state:
-        with pytest.raises(RuntimeError, match="sp_size: 1"):
-            m(x, torch.tensor([500]), ctx, seq_len=4)
+        assert (st.group, st.rank, st.size) == (grp, 2, 4)
+        assert sp.lookup(sp.register(st)) is st
+        assert sp.split_len(73920, st) == 18480
+        with pytest.raises(ValueError, match="divisible"):
+            sp.split_len(10, st)
     else:
-        with pytest.raises(NotImplementedError):
-            m(x, torch.tensor([500]), ctx, seq_len=4)
+        assert st is None and sp.register(st) == 0 and sp.lookup(0) is None
+    try:
+        sp.set_group(False)
+        assert sp.current() is None
+    finally:
+        sp.clear()
