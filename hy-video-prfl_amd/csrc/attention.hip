@@ -526,7 +526,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   constexpr bool PVF = ATTN_FWD_PVFIRST && VT && QS && !SHORT_KV;
   constexpr bool KDX = PVF && ATTN_FWD_KDMA_X && ATTN_G0_DMA_Y;
   constexpr bool SPECPACK = ATTN_SPEC_PACK && QS && ATTN_SUMCHECK;
-  if (PVF) {              // stage 2's V image = zeros for the t = 0 P(-1).V (retired by the barrier)
+  if (PVF) {              // stage 2's V image = zeros for the t = 0 P(-1).V (retired below)
     static_assert(!PVF || SV % (512 * 16) == 0, "zeroing stride");
 #pragma unroll
     for (int i = 0; i < SV / (512 * 16); ++i)
@@ -534,7 +534,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
   }
   if (nkv > 0) dma(0, 0);
   if (nkv > 1) dma(1, 1);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+  // vmcnt(0); with PVF also lgkmcnt(0): the zero stores of stage 2's V image must be retired
+  // before the barrier (gfx950's back-off barrier gets no compiler-inserted wait), since other
+  // waves read that image as the P(-1).V operand of their first MFMA phase
+  __builtin_amdgcn_s_waitcnt(PVF ? 0x0070 : 0x0F70);
   bar();
   if (gp == 1) {          // the lagging (younger) half: one barrier behind, static priority 1
     if (SHORT_KV || ATTN_FWD_PRIO == 1) __builtin_amdgcn_s_setprio(1);

@@ -29,6 +29,8 @@
                         min(1, max_norm/(norm+1e-6)) (`train_prfl.py:825,972`), with the clip
                         coefficient kept on the device (no host synchronisation).
 """
+import weakref
+
 import torch
 
 from . import ops
@@ -38,6 +40,7 @@ class AdamW:
     def __init__(self, params, lr=5e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                  state_on_host=False, ring_slots=3, shard=False, overlap=False):
         self.params = [p for p in params if p.requires_grad]
+        self._orig = list(self.params)      # the caller's order: state_dict indices (attach re-sorts)
         self.shard = shard
         if shard:
             import torch.distributed as dist
@@ -62,19 +65,24 @@ class AdamW:
         self._ready = {}            # param -> event (optimizer stream) after its final write
         self._hooks = []
         # step(zero_grad=True) keeps the gradient buffers (zeroed) where the reference's
-        # optimizer.zero_grad() sets them to None; a parameter whose buffer this optimizer zeroed
-        # and that autograd has not accumulated into since (no gradient in the window) is skipped,
-        # as torch.optim.AdamW skips a None gradient: no weight decay, no moment decay for it
-        self._zeroed = set()
-        self._touched = set()
-        for p in self.params:
-            if p.is_leaf:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._touch))
+        # optimizer.zero_grad() sets them to None.  A parameter whose buffer this optimizer zeroed
+        # and that has received no gradient since is skipped, as torch.optim.AdamW skips a None
+        # gradient (no weight decay, no moment decay).  "Received" is read off the buffer itself:
+        # the zeroed buffer's identity and version counter are recorded, and autograd's in-place
+        # accumulation, `p.grad.copy_(...)` or any in-place write bumps the version while
+        # `p.grad = g` swaps the object — so gradients from hooks, FSDP / ZeRO code or hand-set
+        # ones all count (the zeroing kernel itself writes below the version counter).
+        self._zeroed = {}
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                   params=self.params)]
 
-    def _touch(self, p):
-        self._touched.add(p)
+    def _fresh(self, p):
+        z = self._zeroed.get(p)
+        if z is None:
+            return True
+        ref, ver = z
+        g = p.grad
+        return ref() is not g or g._version != ver
 
     def _host_params(self):
         """The tensors whose moments live on the host: all (state_on_host True), none (False),
@@ -166,17 +174,25 @@ class AdamW:
         one pass): the gradient buffers stay allocated, so the next backward accumulates into
         them instead of allocating 4 B / parameter again while this update may still be reading
         the old ones on the side stream (which made the caching allocator reserve a second set)."""
+        live = [p for p in self.params if p.grad is not None and self._fresh(p)]
+        if (live and live[0].is_cuda and self.overlap and zero_grad
+                and not getattr(self, "_attached", False)):
+            # the next backward accumulates into buffers this update zeroes on the side stream:
+            # only the forward pre-hooks of attach() order that write after the zeroing.  Checked
+            # before any counter moves, so a caller may attach() and call step() again.
+            raise RuntimeError("AdamW(overlap=True).step(zero_grad=True) needs attach(model) first")
         self.step_count += 1
         lr = self.param_groups[0]["lr"]
-        live = [p for p in self.params
-                if p.grad is not None and (p not in self._zeroed or p in self._touched)]
-        self._touched = set()
-        if zero_grad:
-            self._zeroed.update(live)
-        else:
-            self._zeroed.difference_update(live)
         for p in live:
             self._pstep[p] = self._pstep.get(p, 0) + 1
+        self._step_live(live, lr, zero_grad)
+        for p in live:                              # after every in-place write of this step
+            if zero_grad:
+                self._zeroed[p] = (weakref.ref(p.grad), p.grad._version)
+            else:
+                self._zeroed.pop(p, None)
+
+    def _step_live(self, live, lr, zero_grad):
         if not live:
             return
         if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
@@ -190,10 +206,6 @@ class AdamW:
         if self._streams is None:
             self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
         opt, cp = self._streams
-        if self.overlap and zero_grad and not getattr(self, "_attached", False):
-            # the next backward accumulates into buffers this update zeroes on the side stream:
-            # only the forward pre-hooks of attach() order that write after the zeroing
-            raise RuntimeError("AdamW(overlap=True).step(zero_grad=True) needs attach(model) first")
         self.wait(live)                             # a previous step still in flight
         opt.wait_stream(main)                       # grads (clipped) and params are final
         mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
@@ -305,20 +317,45 @@ class AdamW:
     def zero_grad(self, set_to_none=True):
         for p in self.params:
             p.grad = None
-        self._zeroed = set()
-        self._touched = set()
+        self._zeroed = {}
 
     def state_bytes(self):
         return sum(2 * p.numel() * 4 for p in self.state)
 
     def state_dict(self):
-        """Moments of the tensors this rank holds (host or device), by parameter index."""
+        """torch.optim.AdamW's layout: per-parameter {"step", "exp_avg", "exp_avg_sq"} keyed by
+        the index in the CONSTRUCTOR's parameter order (attach() re-sorts the update order, not
+        these keys), one param group; the moments of the tensors this rank holds (host or
+        device; a ZeRO-1 rank holds its own)."""
         self.synchronize()
-        idx = {id(p): i for i, p in enumerate(self.params)}
-        return {"step": self.step_count,
-                "state": {idx[id(p)]: {"step": self._pstep.get(p, 0), "exp_avg": m.view_as(p),
-                                       "exp_avg_sq": v.view_as(p)}
-                          for p, (m, v) in self.state.items()}}
+        idx = {id(p): i for i, p in enumerate(self._orig)}
+        g = {k: v for k, v in self.param_groups[0].items() if k != "params"}
+        g.update(params=list(range(len(self._orig))), amsgrad=False, maximize=False,
+                 foreach=None, capturable=False, differentiable=False, fused=None)
+        return {"state": {idx[id(p)]: {"step": torch.tensor(float(self._pstep.get(p, 0))),
+                                       "exp_avg": m.view_as(p), "exp_avg_sq": v.view_as(p)}
+                          for p, (m, v) in self.state.items()},
+                "param_groups": [g], "prfl_step_count": self.step_count}
+
+    def load_state_dict(self, sd):
+        """Inverse of state_dict (also accepts torch.optim.AdamW's): moments copied into this
+        optimizer's storage (host-pinned or HBM, as this instance places them)."""
+        self.synchronize()
+        for i, st in sd["state"].items():
+            p = self._orig[int(i)]
+            if self.shard and self.owner[p] != self.rank:
+                continue
+            m, v = self._state(p)
+            m.view_as(p).copy_(st["exp_avg"])
+            v.view_as(p).copy_(st["exp_avg_sq"])
+            self._pstep[p] = int(float(st["step"]))
+        self.step_count = int(sd.get("prfl_step_count",
+                                     max([self._pstep.get(p, 0) for p in self._orig] + [0])))
+        g = sd["param_groups"][0]
+        self.param_groups[0].update(lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"],
+                                    weight_decay=g["weight_decay"])
+        self.lr, self.betas, self.eps, self.weight_decay = (g["lr"], tuple(g["betas"]), g["eps"],
+                                                            g["weight_decay"])
 
 
 @torch.no_grad()

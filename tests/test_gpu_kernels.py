@@ -846,8 +846,22 @@ def test_adamw_zero_grad_skips_untouched_like_set_to_none(ops):
 
 
 def test_adamw_overlap_zero_grad_requires_attach(ops):
+    """The refusal comes before any counter moves: after attach() the retried step
+    is the first one, with the bias correction of step 1."""
     from prfl_amd.optim import AdamW
-    p = torch.zeros(8, device=DEV, requires_grad=True)
-    p.grad = torch.ones(8, device=DEV)
+    m = torch.nn.Module()
+    m.blocks = torch.nn.ModuleList([torch.nn.Linear(8, 8, bias=False).to(DEV)])
+    p = m.blocks[0].weight
+    p.grad = torch.ones_like(p)
+    opt = AdamW([p], overlap=True)
     with pytest.raises(RuntimeError, match="attach"):
-        AdamW([p], overlap=True).step(zero_grad=True)
+        opt.step(zero_grad=True)
+    assert opt.step_count == 0 and not opt._pstep and not opt._zeroed
+    twin = p.detach().clone().requires_grad_(True)
+    twin.grad = torch.ones_like(twin)
+    ref = AdamW([twin])
+    opt.attach(m)
+    opt.step(zero_grad=True)
+    ref.step()
+    opt.synchronize()
+    assert opt.step_count == 1 and torch.equal(p, twin)
