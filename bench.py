@@ -354,7 +354,8 @@ def main():
         if prfl:
             # 720p memory plan: the AdamW moments live in pinned host memory and
             # stream through HBM during the step; with DP ranks they are also ZeRO-1 sharded
-            # (each rank holds and streams 1/N of them, then broadcasts the tensors it updated)
+            # (each rank holds and streams 1/N of every parameter group's elements, then one
+            # all-gather per group rebuilds the parameters everywhere)
             big = args.workload.endswith("720") or args.toy
             tr = PRFLTrainer(gen, lrm, qa, mlp, grad_accum=5.0,
                              feature_layer=(TOY_DIMS["lrm_layers"],) if args.toy else (8,),

@@ -21,10 +21,13 @@
                       step's update hides under the reward step's no-grad rollout).  Results are
                       bit-identical to the synchronous update: same kernel, same inputs, and every
                       reader is ordered after the write.
-    ``shard``         (data parallel, world > 1): ZeRO-1 — every rank keeps the moments of, and
-                      updates, only the tensors it owns (size-balanced, the same assignment on
-                      every rank), then each tensor is broadcast from its owner; parameters stay
-                      bit-identical to the replicated update.
+    ``shard``         (data parallel, world > 1): ZeRO-1 — the tensors are grouped (attach(): the
+                      embeddings, each block, the head) and each group, laid end to end, is cut
+                      into `world` equal element shards; rank r keeps the moments of, and
+                      updates, shard r of every group, then one all_gather_into_tensor per group
+                      rebuilds it everywhere (~42 collectives per optimizer step for the 14B DiT
+                      instead of one broadcast per tensor); parameters stay bit-identical to the
+                      replicated update (AdamW is element-wise).
 * ``clip_grad_norm_`` — global L2 norm over all grads and in-place scaling by
                         min(1, max_norm/(norm+1e-6)) (`train_prfl.py:825,972`), with the clip
                         coefficient kept on the device (no host synchronisation).
@@ -38,22 +41,19 @@ from . import ops
 
 class AdamW:
     def __init__(self, params, lr=5e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                 state_on_host=False, ring_slots=3, shard=False, overlap=False):
+                 state_on_host=False, ring_slots=3, shard=False, overlap=False,
+                 shard_bucket_numel=1 << 26):
         self.params = [p for p in params if p.requires_grad]
         self._orig = list(self.params)      # the caller's order: state_dict indices (attach re-sorts)
         self.shard = shard
+        self.rank, self.world = 0, 1
         if shard:
             import torch.distributed as dist
             self.rank, self.world = dist.get_rank(), dist.get_world_size()
-            loads = [0] * self.world
-            self.owner = {}
-            order = sorted(range(len(self.params)), key=lambda i: (-self.params[i].numel(), i))
-            for i in order:
-                r = min(range(self.world), key=lambda k: (loads[k], k))
-                self.owner[self.params[i]] = r
-                loads[r] += self.params[i].numel()
+        self.shard_bucket_numel = shard_bucket_numel
+        self._groups = None         # ZeRO-1 layout (lazy: attach() may still re-order)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
-        self.state = {}
+        self.state = {}             # param -> (exp_avg, exp_avg_sq) of this rank's range of it
         self.step_count = 0         # optimizer steps taken
         self._pstep = {}            # per-parameter update count (torch's state['step']): the bias
         #                             correction of a parameter that skipped a window lags behind
@@ -84,6 +84,49 @@ class AdamW:
         g = p.grad
         return ref() is not g or g._version != ver
 
+    # ------------------------------------------------------------------ ZeRO-1 layout -----
+    def _layout(self):
+        """Groups of tensors in update order, each laid out end to end and cut into `world`
+        equal element shards: rank r updates (and keeps the moments of) shard r of every group,
+        then ONE all_gather_into_tensor per group rebuilds the group on every rank.  Groups are
+        attach()'s (embeddings, each block, the head) or, unattached, consecutive tensors of
+        >= shard_bucket_numel elements.  AdamW is element-wise, so every element gets exactly the
+        update the replicated optimizer computes (same kernel, same per-tensor step count).
+        Without sharding: one group of every tensor, all of it this rank's (no collective).
+
+        self._groups = [(tensors, offsets, n, shard)]; self._range[p] = (a, b) (this rank's
+        elements of p, absent if none)."""
+        if self._groups is not None:
+            return self._groups
+        if not self.shard:
+            lists = [list(self.params)]             # one group: the streamed ring runs end to end
+        elif getattr(self, "_group_lists", None) is not None:
+            lists = [g for g in self._group_lists if g]
+        else:
+            lists, cur, n = [], [], 0
+            for p in self.params:
+                cur.append(p)
+                n += p.numel()
+                if n >= self.shard_bucket_numel:
+                    lists.append(cur)
+                    cur, n = [], 0
+            if cur:
+                lists.append(cur)
+        self._groups, self._range = [], {}
+        for ts in lists:
+            offs, n = [], 0
+            for p in ts:
+                offs.append(n)
+                n += p.numel()
+            sz = -(-n // self.world)
+            lo, hi = self.rank * sz, min(n, (self.rank + 1) * sz)
+            for p, o in zip(ts, offs):
+                a, b = max(lo, o) - o, min(hi, o + p.numel()) - o
+                if a < b:
+                    self._range[p] = (a, b)
+            self._groups.append((ts, offs, n, sz))
+        return self._groups
+
     def _host_params(self):
         """The tensors whose moments live on the host: all (state_on_host True), none (False),
         or the shortest tail of self.params (update order) holding >= f of the parameters."""
@@ -108,19 +151,23 @@ class AdamW:
     def _state(self, p):
         st = self.state.get(p)
         if st is None:
+            self._layout()
+            a, b = self._range[p]
             if p in self._host_params():
-                st = (torch.zeros(p.numel(), dtype=torch.float32, pin_memory=True),
-                      torch.zeros(p.numel(), dtype=torch.float32, pin_memory=True))
+                st = (torch.zeros(b - a, dtype=torch.float32, pin_memory=True),
+                      torch.zeros(b - a, dtype=torch.float32, pin_memory=True))
             else:
-                st = (torch.zeros_like(p), torch.zeros_like(p))
+                st = (torch.zeros(b - a, dtype=torch.float32, device=p.device),
+                      torch.zeros(b - a, dtype=torch.float32, device=p.device))
             self.state[p] = st
         return st
 
     def init_state(self):
         """Allocate the moments now (zeros, as torch.optim.AdamW's lazy first step does) instead
         of inside the first step: pinning 114 GB of host memory takes ~10 s, a one-time cost."""
+        self._layout()
         for p in self.params:
-            if not self.shard or self.owner[p] == self.rank:
+            if p in self._range:
                 self._state(p)
 
     # ------------------------------------------------------------------ ordering ----------
@@ -146,7 +193,8 @@ class AdamW:
         """Forward pre-hooks: each module in `groups` (default: every element of model.blocks,
         then model.head) waits for its own parameters' updates; `model` itself waits for the
         remaining ones (embeddings), which are therefore updated first: the update order becomes
-        [rest, groups...] = the order in which a forward first reads them."""
+        [rest, groups...] = the order in which a forward first reads them.  These are also the
+        ZeRO-1 gather groups (one all-gather each per step)."""
         if groups is None:
             groups = list(model.blocks) + ([model.head] if getattr(model, "head", None) is not None
                                            else [])
@@ -154,12 +202,17 @@ class AdamW:
         rest = [p for p in model.parameters() if id(p) not in inner]
         order = {id(p): i for i, p in enumerate(rest + [p for g in groups for p in g.parameters()])}
         self.params.sort(key=lambda p: order.get(id(p), len(order)))
-        if self.state and self.state_on_host is not True and self.state_on_host is not False:
-            # a fractional host tail is chosen in update order: its moments must not exist yet
-            raise RuntimeError("attach() must precede the first step / init_state() when "
-                               "state_on_host is a fraction: the host tail is chosen in update order")
-        if not self.state:
-            self._host_set = None
+        if self.state:
+            raise RuntimeError("attach() must precede the first step / init_state(): the update "
+                               "order decides the host-moment tail and the ZeRO-1 shards")
+        self._host_set = None
+        mine = {id(p) for p in self.params}
+        lists = [[p for p in rest if id(p) in mine]] + \
+            [[p for p in g.parameters() if id(p) in mine] for g in groups]
+        placed = {id(p) for ts in lists for p in ts}
+        lists.append([p for p in self.params if id(p) not in placed])
+        self._group_lists = lists
+        self._groups = None
         self._hooks.append(model.register_forward_pre_hook(lambda m, a: self.wait(rest)))
         for g in groups:
             ps = list(g.parameters())
@@ -195,54 +248,91 @@ class AdamW:
     def _step_live(self, live, lr, zero_grad):
         if not live:
             return
-        if not live[0].is_cuda:                     # CPU (gloo tests): plain synchronous update
-            self._step_cpu(live, lr)
-            if zero_grad:
-                for p in live:
-                    p.grad.zero_()
-            return
-        dev = live[0].device
-        main = torch.cuda.current_stream(dev)
-        if self._streams is None:
-            self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
-        opt, cp = self._streams
-        self.wait(live)                             # a previous step still in flight
-        opt.wait_stream(main)                       # grads (clipped) and params are final
-        mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
-        with torch.cuda.stream(opt):
-            if zero_grad and self.shard:            # tensors another rank updates
-                for p in live:
-                    if self.owner[p] != self.rank:
+        groups = self._layout()
+        is_live = set(live)
+        cuda = live[0].is_cuda
+        if cuda:
+            dev = live[0].device
+            main = torch.cuda.current_stream(dev)
+            if self._streams is None:
+                self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+            opt, cp = self._streams
+            self.wait(live)                         # a previous step still in flight
+            opt.wait_stream(main)                   # grads (clipped) and params are final
+        host = self._host_params()
+        for ts, offs, n, sz in groups:
+            glive = [p for p in ts if p in is_live]
+            if not glive:
+                continue
+            units = [(p,) + self._range[p] for p in glive if p in self._range]
+            if not cuda:                            # CPU (gloo tests): plain synchronous update
+                self._update_cpu(units, lr)
+                if zero_grad:
+                    for p in glive:
                         p.grad.zero_()
-            host = self._host_params()
-            # device-resident moments first (the earlier tensors in update order), then the
-            # streamed tail: its first H2D copies start on `cp` at once, beside the device updates
-            done = self._update_device([p for p in mine if p not in host], lr, zero_grad)
-            done.update(self._update_streamed([p for p in mine if p in host], lr, opt, cp,
-                                              zero_grad))
-            if self.shard:
-                import torch.distributed as dist
-                for p in live:
-                    if p in done:
-                        opt.wait_event(done[p])
-                    dist.broadcast(p.data, src=self.owner[p], async_op=True).wait()
+                self._gather(ts, offs, n, sz, is_live)
+                continue
+            with torch.cuda.stream(opt):
+                if zero_grad and self.shard:        # the elements another rank updates
+                    for p in glive:
+                        a, b = self._range.get(p, (0, 0))
+                        g = p.grad.view(-1)
+                        if a > 0:
+                            g[:a].zero_()
+                        if b < g.numel():
+                            g[b:].zero_()
+                # device-resident moments first, then the streamed ones: their first H2D copies
+                # start on `cp` at once, beside the device updates
+                done = self._update_device([u for u in units if u[0] not in host], lr, zero_grad)
+                done.update(self._update_streamed([u for u in units if u[0] in host], lr, opt, cp,
+                                                  zero_grad))
+                if self.shard:
+                    for p in glive:
+                        if p in done:
+                            opt.wait_event(done[p])
+                    self._gather(ts, offs, n, sz, is_live)
                     ev = torch.cuda.Event()
                     ev.record(opt)
-                    self._ready[p] = ev
-            else:
-                self._ready.update(done)
-        for p in live:                              # grads are read on the side stream
-            p.grad.record_stream(opt)
-        if not self.overlap:
-            self.wait(live)
+                    for p in glive:
+                        self._ready[p] = ev
+                else:
+                    self._ready.update(done)
+        if cuda:
+            for p in live:                          # grads are read on the side stream
+                p.grad.record_stream(opt)
+            if not self.overlap:
+                self.wait(live)
 
-    def _update_device(self, live, lr, zero_grad=False):
+    def _gather(self, ts, offs, n, sz, is_live):
+        """ZeRO-1: this rank's updated shard of the group -> every rank (one collective)."""
+        if not self.shard:
+            return
+        import torch.distributed as dist
+        dev = ts[0].device
+        lo = self.rank * sz
+        shard = torch.empty(sz, dtype=torch.float32, device=dev)
+        for p, o in zip(ts, offs):
+            r = self._range.get(p)
+            if r is not None and p in is_live:      # (other slots: not read back below)
+                shard[o + r[0] - lo:o + r[1] - lo].copy_(p.data.view(-1)[r[0]:r[1]])
+        full = torch.empty(sz * self.world, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(full, shard, async_op=True).wait()
+        for p, o in zip(ts, offs):
+            if p in is_live:
+                p.data.view(-1).copy_(full[o:o + p.numel()])
+
+    @staticmethod
+    def _flat(t, a, b):
+        return t.view(-1)[a:b]
+
+    def _update_device(self, units, lr, zero_grad=False):
         done = {}
-        for p in live:
+        for p, a, b in units:
             m, v = self._state(p)
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            ops.adamw_(p.data, g, m, v, lr, self.betas[0], self.betas[1], self.eps,
-                       self.weight_decay, self._pstep[p], zero_grad=zero_grad)
+            ops.adamw_(self._flat(p.data, a, b), self._flat(g, a, b), m, v, lr, self.betas[0],
+                       self.betas[1], self.eps, self.weight_decay, self._pstep[p],
+                       zero_grad=zero_grad)
             if zero_grad and g is not p.grad:
                 p.grad.zero_()
             ev = torch.cuda.Event()
@@ -250,44 +340,45 @@ class AdamW:
             done[p] = ev
         return done
 
-    def _update_streamed(self, live, lr, opt, cp, zero_grad=False):
+    def _update_streamed(self, units, lr, opt, cp, zero_grad=False):
         """Moments host -> ring -> kernel -> host, one copy stream for both directions: copy
         stream order H2D(0..k-1), then per tensor i: D2H(i) after kernel(i), H2D(i+k) into the
         slot D2H(i) just drained."""
         done = {}
-        if not live:
+        if not units:
             return done
-        dev = live[0].device
-        nmax = max(p.numel() for p in live)
+        dev = units[0][0].device
+        nmax = max(b - a for _, a, b in units)
         k = self.ring_slots
         if self._ring is None or self._ring[0].numel() < 2 * nmax:
             self._ring = [torch.empty(2 * nmax, dtype=torch.float32, device=dev) for _ in range(k)]
-            for b in self._ring:
-                b.record_stream(cp)
-        slots = [(b[:nmax], b[nmax:2 * nmax]) for b in self._ring]
-        h2d_ev = [None] * len(live)
+            for buf in self._ring:
+                buf.record_stream(cp)
+        cap = self._ring[0].numel() // 2
+        slots = [(buf[:cap], buf[cap:2 * cap]) for buf in self._ring]
+        h2d_ev = [None] * len(units)
 
         def h2d(i):
-            p = live[i]
+            p, a, b = units[i]
             m_h, v_h = self._state(p)
             m_d, v_d = slots[i % k]
-            n = p.numel()
+            n = b - a
             with torch.cuda.stream(cp):
                 m_d[:n].copy_(m_h, non_blocking=True)
                 v_d[:n].copy_(v_h, non_blocking=True)
                 h2d_ev[i] = torch.cuda.Event()
                 h2d_ev[i].record(cp)
 
-        # the ring is reused across steps: the previous step's D2H are earlier on `cp`
-        for i in range(min(k, len(live))):
+        # the ring is reused across steps and groups: earlier D2H copies are earlier on `cp`
+        for i in range(min(k, len(units))):
             h2d(i)
-        for i, p in enumerate(live):
-            n = p.numel()
+        for i, (p, a, b) in enumerate(units):
+            n = b - a
             m_d, v_d = slots[i % k]
             opt.wait_event(h2d_ev[i])
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            ops.adamw_(p.data, g, m_d[:n].view_as(p), v_d[:n].view_as(p), lr, self.betas[0],
-                       self.betas[1], self.eps, self.weight_decay, self._pstep[p],
+            ops.adamw_(self._flat(p.data, a, b), self._flat(g, a, b), m_d[:n], v_d[:n], lr,
+                       self.betas[0], self.betas[1], self.eps, self.weight_decay, self._pstep[p],
                        zero_grad=zero_grad)
             if zero_grad and g is not p.grad:
                 p.grad.zero_()
@@ -299,20 +390,15 @@ class AdamW:
                 cp.wait_event(ev)
                 m_h.copy_(m_d[:n], non_blocking=True)
                 v_h.copy_(v_d[:n], non_blocking=True)
-            if i + k < len(live):
+            if i + k < len(units):
                 h2d(i + k)
         return done
 
-    def _step_cpu(self, live, lr):
-        mine = [p for p in live if not self.shard or self.owner[p] == self.rank]
-        for p in mine:
+    def _update_cpu(self, units, lr):
+        for p, a, b in units:
             m, v = self._state(p)
-            ops.adamw_(p.data, p.grad, m, v, lr, self.betas[0], self.betas[1], self.eps,
-                       self.weight_decay, self._pstep[p])
-        if self.shard:
-            import torch.distributed as dist
-            for p in live:
-                dist.broadcast(p.data, src=self.owner[p])
+            ops.adamw_(self._flat(p.data, a, b), self._flat(p.grad, a, b), m, v, lr, self.betas[0],
+                       self.betas[1], self.eps, self.weight_decay, self._pstep[p])
 
     def zero_grad(self, set_to_none=True):
         for p in self.params:
@@ -320,35 +406,47 @@ class AdamW:
         self._zeroed = {}
 
     def state_bytes(self):
-        return sum(2 * p.numel() * 4 for p in self.state)
+        return sum(2 * m.numel() * 4 for m, _ in self.state.values())
 
     def state_dict(self):
         """torch.optim.AdamW's layout: per-parameter {"step", "exp_avg", "exp_avg_sq"} keyed by
         the index in the CONSTRUCTOR's parameter order (attach() re-sorts the update order, not
-        these keys), one param group; the moments of the tensors this rank holds (host or
-        device; a ZeRO-1 rank holds its own)."""
+        these keys), one param group.  Unsharded every entry is torch-loadable; a ZeRO-1 rank
+        holds its element range of some tensors: those entries carry "range" = (a, b) and flat
+        moments (this class's load_state_dict reads them on a rank of the same layout)."""
         self.synchronize()
         idx = {id(p): i for i, p in enumerate(self._orig)}
         g = {k: v for k, v in self.param_groups[0].items() if k != "params"}
         g.update(params=list(range(len(self._orig))), amsgrad=False, maximize=False,
                  foreach=None, capturable=False, differentiable=False, fused=None)
-        return {"state": {idx[id(p)]: {"step": torch.tensor(float(self._pstep.get(p, 0))),
-                                       "exp_avg": m.view_as(p), "exp_avg_sq": v.view_as(p)}
-                          for p, (m, v) in self.state.items()},
-                "param_groups": [g], "prfl_step_count": self.step_count}
+        st = {}
+        for p, (m, v) in self.state.items():
+            a, b = self._range[p]
+            whole = (a, b) == (0, p.numel())
+            e = {"step": torch.tensor(float(self._pstep.get(p, 0))),
+                 "exp_avg": m.view_as(p) if whole else m, "exp_avg_sq": v.view_as(p) if whole else v}
+            if not whole:
+                e["range"] = (a, b)
+            st[idx[id(p)]] = e
+        return {"state": st, "param_groups": [g], "prfl_step_count": self.step_count}
 
     def load_state_dict(self, sd):
         """Inverse of state_dict (also accepts torch.optim.AdamW's): moments copied into this
         optimizer's storage (host-pinned or HBM, as this instance places them)."""
         self.synchronize()
-        for i, st in sd["state"].items():
+        self._layout()
+        for i, e in sd["state"].items():
             p = self._orig[int(i)]
-            if self.shard and self.owner[p] != self.rank:
+            if p not in self._range:
                 continue
+            a, b = self._range[p]
+            if tuple(e.get("range", (0, p.numel()))) != (a, b):
+                raise ValueError(f"state_dict entry {i}: element range {e.get('range')} does not "
+                                 f"match this rank's {(a, b)} (different ZeRO-1 layout)")
             m, v = self._state(p)
-            m.view_as(p).copy_(st["exp_avg"])
-            v.view_as(p).copy_(st["exp_avg_sq"])
-            self._pstep[p] = int(float(st["step"]))
+            m.copy_(e["exp_avg"].reshape(-1))
+            v.copy_(e["exp_avg_sq"].reshape(-1))
+            self._pstep[p] = int(float(e["step"]))
         self.step_count = int(sd.get("prfl_step_count",
                                      max([self._pstep.get(p, 0) for p in self._orig] + [0])))
         g = sd["param_groups"][0]

@@ -86,20 +86,23 @@ def _zero1_worker(rank, world, port, out_q):
     optim.ops.adamw_ = _adamw_ref
     torch.manual_seed(0)
     ps = [torch.randn(s).requires_grad_(True) for s in [(64, 33), (1000,), (7,), (300, 3), (5, 5)]]
-    opt = optim.AdamW(ps, lr=1e-2, shard=True)
+    # a bucket of ~1500 elements: groups [(64, 33)], [(1000,), (7,), (300, 3)], [(5, 5)] -> every
+    # element shard boundary falls inside a tensor somewhere
+    opt = optim.AdamW(ps, lr=1e-2, shard=True, shard_bucket_numel=1500)
     g = torch.Generator().manual_seed(1)
     for _ in range(3):
         for p in ps:
             p.grad = torch.randn(p.shape, generator=g)    # identical on both ranks (post all-reduce)
         opt.step()
-    owned = sorted(i for i, p in enumerate(ps) if opt.owner[p] == rank)
-    out_q.put((rank, [p.detach().numpy().copy() for p in ps], owned, len(opt.state)))
+    owned = {i: opt._range[p] for i, p in enumerate(ps) if p in opt._range}
+    out_q.put((rank, [p.detach().numpy().copy() for p in ps], owned, opt.state_bytes() // 8))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_zero1_adamw_gloo_world2():
-    """ZeRO-1 AdamW: each rank holds half the moments; parameters equal the replicated update."""
+    """ZeRO-1 AdamW (element shards of each group, one all-gather per group): each rank holds half
+    the moments; parameters equal the replicated update bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 30500 + os.getpid() % 1000
@@ -110,8 +113,14 @@ def test_zero1_adamw_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     (_, p0, own0, n0), (_, p1, own1, n1) = res
-    assert sorted(own0 + own1) == list(range(5)) and not set(own0) & set(own1)
-    assert n0 == len(own0) and n1 == len(own1)
+    shapes = [(64, 33), (1000,), (7,), (300, 3), (5, 5)]
+    numel = [int(torch.Size(s).numel()) for s in shapes]
+    # every element owned by exactly one rank, moments only for the owned elements
+    for i, n in enumerate(numel):
+        cover = sorted([own0[i]] if i in own0 else []) + sorted([own1[i]] if i in own1 else [])
+        assert sum(b - a for a, b in cover) == n, (i, cover)
+    assert n0 + n1 == sum(numel) and abs(n0 - n1) <= 3
+    assert any(i in own0 and i in own1 for i in range(5))      # a tensor split between ranks
     torch.manual_seed(0)
     ref = [torch.randn(s) for s in [(64, 33), (1000,), (7,), (300, 3), (5, 5)]]
     st = [(torch.zeros_like(p), torch.zeros_like(p)) for p in ref]
@@ -222,7 +231,7 @@ def test_nan_loss_skip_is_agreed_across_ranks_world2():
 # RCCL (like NCCL) needs every rank to issue the same collectives in the same order: the
 # GradReducer's all-reduces (post-accumulate hooks, in autograd's order, then the coalesced small
 # tensors at end()), the guard's MAX flag, the loss averages, mid_timestep's broadcast and the
-# ZeRO-1 per-tensor broadcasts from the optimizer step.  The toy modules below stand in for the
+# ZeRO-1 per-group all-gathers from the optimizer step.  The toy modules below stand in for the
 # HIP-backed WanModel (which has no CPU path) behind the same call signature; the compute ops the
 # trainer calls directly (UniPC update, clip, AdamW) are swapped for their torch restatements.
 
@@ -266,8 +275,11 @@ class _ToyQA(torch.nn.Module):
         return self.q(feats.mean(dim=(0, 2)))
 
 
+_RECORDED = ("all_reduce", "broadcast", "all_gather_into_tensor")
+
+
 def _record_collectives(log):
-    real = {n: getattr(dist, n) for n in ("all_reduce", "broadcast")}
+    real = {n: getattr(dist, n) for n in _RECORDED}
 
     def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
         log.append(("all_reduce", tuple(t.shape), str(t.dtype), str(op)))
@@ -276,7 +288,12 @@ def _record_collectives(log):
     def broadcast(t, src=0, group=None, async_op=False):
         log.append(("broadcast", tuple(t.shape), str(t.dtype), int(src)))
         return real["broadcast"](t, src=src, group=group, async_op=async_op)
+
+    def all_gather_into_tensor(out, inp, group=None, async_op=False):
+        log.append(("all_gather_into_tensor", tuple(out.shape), str(out.dtype), tuple(inp.shape)))
+        return real["all_gather_into_tensor"](out, inp, group=group, async_op=async_op)
     dist.all_reduce, dist.broadcast = all_reduce, broadcast
+    dist.all_gather_into_tensor = all_gather_into_tensor
     return real
 
 
@@ -313,21 +330,23 @@ def _trainer_worker(rank, world, port, out_q):
     for step in range(4):                              # two iterations, each SFT + reward; GA 2
         tr.sft_step(step, latents, text, 32, generator=g)
         mids.append(tr.reward_step(step, latents, text, 32, generator=g)["mid"])
-    dist.all_reduce, dist.broadcast = real["all_reduce"], real["broadcast"]
-    loads = [0] * world
-    for p, r in tr.optimizer.owner.items():
-        loads[r] += p.numel()
-    out_q.put((rank, log, mids, loads, max(p.numel() for p in tr.params),
-               [p.detach().numpy().copy() for p in gen.parameters()], len(tr.optimizer.state)))
+    for n in _RECORDED:
+        setattr(dist, n, real[n])
+    opt = tr.optimizer
+    mine = sum(b - a for a, b in opt._range.values())
+    out_q.put((rank, log, mids, mine, len(opt._layout()),
+               [p.detach().numpy().copy() for p in gen.parameters()], opt.state_bytes() // 8,
+               sum(p.numel() for p in tr.params)))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_prfl_trainer_collective_sequence_identical_world4():
-    """four ranks run two PRFL iterations (SFT + reward, gradient accumulation 2,
-    ZeRO-1 with overlap=True) through PRFLTrainer; every rank must issue the identical collective
-    sequence (op, shape, dtype, reduce-op / root), the replicas must stay identical, rank 0's
-    mid_timestep must reach every rank, and the ZeRO-1 ownership must be size-balanced."""
+    """four ranks run two PRFL iterations (SFT + reward, gradient
+    accumulation 2, ZeRO-1 with overlap=True) through PRFLTrainer; every rank must issue the
+    identical collective sequence (op, shape, dtype, reduce-op / root), the replicas must stay
+    identical, rank 0's mid_timestep must reach every rank, and ZeRO-1 must take one all-gather
+    per parameter group (<= 60 per optimizer step) over balanced element shards."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     world = 4
@@ -344,16 +363,21 @@ def test_prfl_trainer_collective_sequence_identical_world4():
         assert logs[r] == logs[0], f"rank {r} diverges at collective " \
             f"{next(i for i, (a, b) in enumerate(zip(logs[r], logs[0])) if a != b)}"
     kinds = {e[0] for e in logs[0]}
-    assert kinds == {"all_reduce", "broadcast"}
-    # one ZeRO-1 broadcast per trainable tensor per optimizer step (steps 1 and 3: two per step)
-    n_params = len(res[0][5])
-    roots = [e[3] for e in logs[0] if e[0] == "broadcast" and e[1] != (1,)]
-    assert len(roots) == 2 * 2 * n_params and set(roots) == set(range(world))
+    assert kinds == {"all_reduce", "broadcast", "all_gather_into_tensor"}
+    # ZeRO-1: ONE all-gather per group (embeddings, each block, the head) per optimizer update —
+    # two optimizer steps per iteration (SFT + reward at GA boundaries), two iterations — and
+    # no per-tensor broadcast any more (the broadcasts left are mid_timestep's, shape (1,))
+    n_groups = res[0][4]
+    gathers = [e for e in logs[0] if e[0] == "all_gather_into_tensor"]
+    assert len(gathers) == 2 * 2 * n_groups and n_groups <= 60
+    assert all(e[1] == (1,) for e in logs[0] if e[0] == "broadcast")
+    print(f"collectives over 2 iterations: {len(logs[0])} ({len(gathers)} ZeRO-1 all-gathers, "
+          f"{n_groups} groups per optimizer step)")
     mids = [r[2] for r in res]
     assert all(m == mids[0] for m in mids)
-    loads, biggest = res[0][3], res[0][4]
-    assert max(loads) - min(loads) <= biggest, loads
-    assert sum(r[6] for r in res) == n_params         # each tensor's moments on exactly one rank
+    mine, total = [r[3] for r in res], res[0][7]
+    assert sum(mine) == total and max(mine) - min(mine) <= n_groups, mine   # balanced shards
+    assert sum(r[6] for r in res) == total            # each element's moments on exactly one rank
     for r in range(1, world):
         for a, b in zip(res[r][5], res[0][5]):
             assert torch.equal(a, b)
