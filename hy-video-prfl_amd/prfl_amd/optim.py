@@ -202,9 +202,11 @@ class AdamW:
         rest = [p for p in model.parameters() if id(p) not in inner]
         order = {id(p): i for i, p in enumerate(rest + [p for g in groups for p in g.parameters()])}
         self.params.sort(key=lambda p: order.get(id(p), len(order)))
-        if self.state:
-            raise RuntimeError("attach() must precede the first step / init_state(): the update "
-                               "order decides the host-moment tail and the ZeRO-1 shards")
+        if self.step_count:
+            raise RuntimeError("attach() must precede the first step: the update order decides "
+                               "the host-moment tail and the ZeRO-1 shards")
+        reinit = bool(self.state)           # zero moments from init_state(): re-placed below
+        self.state = {}
         self._host_set = None
         mine = {id(p) for p in self.params}
         lists = [[p for p in rest if id(p) in mine]] + \
@@ -213,6 +215,8 @@ class AdamW:
         lists.append([p for p in self.params if id(p) not in placed])
         self._group_lists = lists
         self._groups = None
+        if reinit:
+            self.init_state()
         self._hooks.append(model.register_forward_pre_hook(lambda m, a: self.wait(rest)))
         for g in groups:
             ps = list(g.parameters())

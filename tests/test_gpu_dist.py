@@ -86,7 +86,7 @@ def test_zero1_streamed_overlapped_adamw_two_ranks_one_gpu():
         p.join(timeout=60)
     (_, p0, l0, n0), (_, p1, l1, n1) = res
     # moments split between ranks: element shards of each group (emb, 3 blocks, head)
-    assert n0 + n1 == sum(a.size for a in p0) and n0 > 0 and n1 > 0
+    assert n0 + n1 == sum(a.numel() for a in p0) and n0 > 0 and n1 > 0
     # replicated reference: same model, synchronous on-device AdamW, one process
     torch.manual_seed(0)
     model = _Toy().cuda()
