@@ -246,11 +246,203 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
   }
 }
 
+// ---- RMSNorm + RoPE, one wave per row (round 6, RMS_WAVE) ------------------------------------
+// 16-B loads and stores (8 bf16 per chunk, chunk c = lane + 64 j), the row held in registers, the
+// sum of squares a wave shuffle (no workgroup barrier per row), w staged once per workgroup in LDS
+// (the 256-thread form re-read 20 KB of fp32 w from L2 for every 10 KB row), and the RoPE
+// multipliers loaded once per row: a lane's chunks all start at the same element of a head
+// ((lane * 8) & 127), so its 4 (cos, sin) pairs are the same for every chunk of the row.
+// Per-element arithmetic as rms_rope_fwd_kernel; only the order of the row's sum of squares
+// differs (fp32 rounding of rstd).
+#ifndef RMS_WAVE
+#define RMS_WAVE 1
+#endif
+constexpr int RW_RPW = 4;     // rows per wave in the forward (16 rows per workgroup)
+constexpr int RW_NJ = 10;     // 16-B chunks per lane: C <= 64 * 10 * 8 = 5120
+
+__device__ __forceinline__ void rope_cs4(const float2* __restrict__ tab, int pair0, int pf, int ph,
+                                         int pw, float2 (&cs)[4]) {
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) cs[pp] = tab[rope_index(pair0 + pp, pf, ph, pw) * 64 + pair0 + pp];
+}
+
+__global__ __launch_bounds__(NT) void rms_rope_fwd_wave_kernel(
+    const bf16* __restrict__ x, int64_t ldx, int L, int C, const float* __restrict__ w, float eps,
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ out,
+    int64_t ldo, float* __restrict__ rstd_out, float oscale) {
+  __shared__ f32x4 ws[RW_NJ * 64 * 2];
+  for (int c = threadIdx.x; c < C / 4; c += NT) ws[c] = ldf4(w, c * 4);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, nc = C / 8, pair0 = ((lane * 8) & 127) >> 1;
+  const int64_t rbase = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RW_RPW;
+  for (int rr = 0; rr < RW_RPW; ++rr) {
+    const int64_t row = rbase + rr;
+    if (row >= L) return;
+    bf16x8 v[RW_NJ];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < RW_NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc) {
+        v[j] = *(const bf16x8*)(x + row * ldx + c * 8);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ss += bf2f(v[j][r]) * bf2f(v[j][r]);
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / C + eps);
+    int pf, ph, pw;
+    bool rot;
+    rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
+    rot = rot && tab != nullptr;
+    float2 cs[4];
+    if (rot) rope_cs4(tab, pair0, pf, ph, pw, cs);
+#pragma unroll
+    for (int j = 0; j < RW_NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc) {
+        const f32x4 w0 = ws[2 * c], w1 = ws[2 * c + 1];
+        float y[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          y[r] = mul_rn(bfr(bf2f(v[j][r]) * rstd), w0[r]);
+          y[r + 4] = mul_rn(bfr(bf2f(v[j][r + 4]) * rstd), w1[r]);
+        }
+        bf16x8 o;
+        if (rot) {
+#pragma unroll
+          for (int pp = 0; pp < 4; ++pp) {
+            const float a = y[2 * pp], bq = y[2 * pp + 1];
+            o[2 * pp] = f2bf(__fmul_rn(__fsub_rn(__fmul_rn(a, cs[pp].x), __fmul_rn(bq, cs[pp].y)), oscale));
+            o[2 * pp + 1] = f2bf(__fmul_rn(__fadd_rn(__fmul_rn(a, cs[pp].y), __fmul_rn(bq, cs[pp].x)), oscale));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = f2bf(__fmul_rn(y[r], oscale));
+        }
+        *(bf16x8*)(out + row * ldo + c * 8) = o;
+      }
+    }
+    if (lane == 0) rstd_out[row] = rstd;
+  }
+}
+
+// backward: the workgroup's BWD_ROWS rows, wave k taking rows k, k + 4, ...; 16-B chunks, the
+// d w partial kept per lane (80 registers) and summed over
+// the four waves in LDS in a fixed order (deterministic), one partial row per workgroup as before
+template <int ROWS>
+__global__ __launch_bounds__(NT) void rms_rope_bwd_wave_kernel(
+    const bf16* __restrict__ dout, int64_t lddo, const bf16* __restrict__ x, int64_t ldx,
+    const float* __restrict__ rstd_in, int L, int C, const float* __restrict__ w,
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ dx,
+    int64_t lddx, float* __restrict__ part0, float oscale) {
+  __shared__ f32x4 ws[RW_NJ * 64 * 2];
+  __shared__ f32x4 acc[RW_NJ * 64 * 2];
+  for (int c = threadIdx.x; c < C / 4; c += NT) ws[c] = ldf4(w, c * 4);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nc = C / 8;
+  const int pair0 = ((lane * 8) & 127) >> 1;
+  float p0[RW_NJ][8];
+#pragma unroll
+  for (int j = 0; j < RW_NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) p0[j][r] = 0.f;
+  for (int rr = wv; rr < ROWS; rr += NT / 64) {
+    const int64_t row = (int64_t)blockIdx.x * ROWS + rr;
+    if (row >= L) break;
+    const float rstd = rstd_in[row];
+    int pf, ph, pw;
+    bool rot;
+    rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
+    rot = rot && tab != nullptr;
+    float2 cs[4];
+    if (rot) rope_cs4(tab, pair0, pf, ph, pw, cs);
+    // pass 1 streams the row from HBM; pass 2 re-reads it (L1 / L2) rather than holding both
+    // operands across the row reduction beside the 80 partial sums (305 registers, 1 wave / SIMD)
+    auto dyv = [&](const bf16x8& gq, float (&dy)[8]) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dy[r] = bf2f(gq[r]) * oscale;
+      if (rot) {
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const float ga = dy[2 * pp], gb = dy[2 * pp + 1];
+          dy[2 * pp] = ga * cs[pp].x + gb * cs[pp].y;
+          dy[2 * pp + 1] = gb * cs[pp].x - ga * cs[pp].y;
+        }
+      }
+    };
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < RW_NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc) {
+        const bf16x8 gq = *(const bf16x8*)(dout + row * lddo + c * 8);
+        const bf16x8 xq = *(const bf16x8*)(x + row * ldx + c * 8);
+        float dy[8];
+        dyv(gq, dy);
+        const f32x4 w0 = ws[2 * c], w1 = ws[2 * c + 1];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float xhat = bf2f(xq[r]) * rstd;
+          const float d = bfr(dy[r] * (r < 4 ? w0[r] : w1[r - 4]));
+          p0[j][r] += dy[r] * bfr(xhat);
+          s += d * xhat;
+        }
+      }
+    }
+    const float m = wave_sum(s) / C;
+#pragma unroll
+    for (int j = 0; j < RW_NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc) {
+        const bf16x8 gq = *(const bf16x8*)(dout + row * lddo + c * 8);
+        const bf16x8 xq = *(const bf16x8*)(x + row * ldx + c * 8);
+        float dy[8];
+        dyv(gq, dy);
+        const f32x4 w0 = ws[2 * c], w1 = ws[2 * c + 1];
+        bf16x8 o;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float xhat = bf2f(xq[r]) * rstd;
+          const float d = bfr(dy[r] * (r < 4 ? w0[r] : w1[r - 4]));
+          o[r] = f2bf(rstd * (d - xhat * m));
+        }
+        *(bf16x8*)(dx + row * lddx + c * 8) = o;
+      }
+    }
+  }
+  // sum the four waves' partials in a fixed order: wave 0 stores, waves 1..3 add in turn
+  for (int k = 0; k < NT / 64; ++k) {
+    if (wv == k) {
+#pragma unroll
+      for (int j = 0; j < RW_NJ; ++j) {
+        const int c = lane + 64 * j;
+        if (c < nc) {
+          const f32x4 a = {p0[j][0], p0[j][1], p0[j][2], p0[j][3]};
+          const f32x4 b = {p0[j][4], p0[j][5], p0[j][6], p0[j][7]};
+          if (k == 0) {
+            acc[2 * c] = a;
+            acc[2 * c + 1] = b;
+          } else {
+            acc[2 * c] = acc[2 * c] + a;
+            acc[2 * c + 1] = acc[2 * c + 1] + b;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < C / 4; c += NT)
+    *(f32x4*)(part0 + (int64_t)blockIdx.x * C + c * 4) = acc[c];
+}
+
 // LN + modulate forward: one wave per row, the row (C <= 5120 -> 20 float4 chunks per lane) held
 // in registers, both reductions wave shuffles (two-pass mean / variance); the per-column
 // coefficients — (1 + scale, shift) or (w, b) — are staged once per workgroup in LDS and each wave
 // normalises RPW rows in turn (re-reading them from L2 per row cost 8 B for every 4 B of x).
-constexpr int RPW = 4;   // rows per wave -> 16 rows per workgroup
+#ifndef LN_RPW
+#define LN_RPW 4
+#endif
+constexpr int RPW = LN_RPW;   // rows per wave -> 16 rows per workgroup
 __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
     const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ w,
@@ -323,6 +515,11 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
 
 constexpr int BWD_ROWS = 32;
 bool bad_c(int64_t C) { return C <= 0 || (C % 4) != 0 || C > 4 * MAXV * NT; }
+// the one-wave-per-row RMSNorm+RoPE kernels: 16-B chunks of both row-major operands
+bool wave_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int64_t C) {
+  return C % 8 == 0 && C <= 64 * RW_NJ * 8 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
+}
 }  // namespace
 
 extern "C" int prfl_norm_rows_per_part(void) { return BWD_ROWS; }
@@ -370,11 +567,19 @@ extern "C" int prfl_rms_rope_fwd_pos(const void* x, int64_t ldx, int64_t L, int6
   if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
-  // (a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p:
-  // profiles/r03_ab_rms_rope_wave.txt)
-  hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C, w,
-                     eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)out, ldo,
-                     rstd, out_scale);
+  // (round 3: a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p,
+  // profiles/r03_ab_rms_rope_wave.txt; round 6's RMS_WAVE form adds 16-B chunks, w in LDS and
+  // several rows per wave: profiles/r06_ab_norms.txt)
+  if (RMS_WAVE && wave_ok(x, ldx, out, ldo, C)) {
+    const int64_t rows = NT / 64 * RW_RPW;
+    hipLaunchKernelGGL(rms_rope_fwd_wave_kernel, dim3((L + rows - 1) / rows), dim3(NT), 0, s,
+                       (const bf16*)x, ldx, (int)L, (int)C, w, eps, (const float2*)rope_tab, (int)F,
+                       (int)Hg, (int)Wg, row0, (bf16*)out, ldo, rstd, out_scale);
+  } else {
+    hipLaunchKernelGGL(rms_rope_fwd_kernel, dim3(L), dim3(NT), 0, s, (const bf16*)x, ldx, (int)C,
+                       w, eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)out,
+                       ldo, rstd, out_scale);
+  }
   prfl_prof::set_work((double)L * C * 4);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();
@@ -390,10 +595,17 @@ extern "C" int prfl_rms_rope_bwd_pos(const void* dout, int64_t lddo, const void*
   if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
-  hipLaunchKernelGGL(rms_rope_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
-                     0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L, (int)C, w,
-                     (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)dx, lddx,
-                     part0, out_scale);
+  if (RMS_WAVE && wave_ok(x, ldx, dx, lddx, C) && wave_ok(dout, lddo, dout, lddo, C)) {
+    hipLaunchKernelGGL(rms_rope_bwd_wave_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS),
+                       dim3(NT), 0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L,
+                       (int)C, w, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0,
+                       (bf16*)dx, lddx, part0, out_scale);
+  } else {
+    hipLaunchKernelGGL(rms_rope_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS),
+                       dim3(NT), 0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L,
+                       (int)C, w, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0,
+                       (bf16*)dx, lddx, part0, out_scale);
+  }
   prfl_prof::set_work((double)L * C * 6);
   prfl_prof::end(KID_RMS, s);
   PRFL_LAUNCH_CHECK();

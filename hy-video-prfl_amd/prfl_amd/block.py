@@ -74,14 +74,38 @@ class Meta:
         # Ulysses sequence parallelism (sp.SPState or None): x holds this rank's L tokens, the
         # rank's tokens start at position sp.rank * L of the padded sequence (sp.py)
         self.sp = sp
-        # config C5 (WanModel.set_fp8_gemm): 0 bf16; 1 e4m3 forward projections; 2 also the e4m3
-        # self-attention forward (ops.attn_fwd_fp8; its backward stays bf16 on that forward's O/LSE)
+        # config C5 (WanModel.set_fp8_gemm): fp8 & 3 = 0 bf16; 1 e4m3 forward projections; 2 also
+        # the e4m3 self-attention forward (ops.attn_fwd_fp8; its backward stays bf16 on that
+        # forward's O/LSE); fp8 >> 2 = mask of projections kept bf16 (fp8_code)
         self.fp8 = int(fp8)
+        self.fp8_mode = self.fp8 & 3
         self.grid = grid            # list of (F, H, W) per sample
         self.seq_len = seq_len      # list of valid key lengths per sample (k_lens)
         self.rope_tab = rope_tab    # fp32 [1024, 64, 2] device tensor
         self.i2v = i2v
         self.eps = eps
+
+
+PROJ = ("qkv", "o", "cq", "co", "1", "2")   # the six forward projections the fp8 path quantises
+
+
+def fp8_code(mode, keep_bf16=()):
+    """The `fp8` integer of Meta / the prfl::wan_block op: mode 0 / 1 / 2 (block.Meta) plus the
+    projections (names of PROJ) that stay bf16 while the others run e4m3 — the per-projection
+    error study of config C5 (tests/test_gpu_fp8.py) and its bf16-kept option."""
+    mask = 0
+    for n in keep_bf16:
+        mask |= 1 << PROJ.index(n)
+    return int(mode) | (mask << 2)
+
+
+# config C5's default (round 6): the cross-attention q / o projections stay bf16.  Measured on the
+# real-width I2V block against the fp32 truth (profiles/r06_c5_projection_table.log), e4m3 on ONE
+# operand at a time gives a residual-update error of 3.3 % (cross q), 3.4 % (cross o), 1.8 %
+# (FFN up / down), 0.7 % (QKV, self o, the int8 / e4m3 attention: the bf16 path's own 0.6 %);
+# all of them together 5.3 %, with cross q + o bf16 2.5 % (SURVEY §8c's 5e-2), for the
+# bf16 cost of two C x C GEMMs per block forward
+C5_KEEP_BF16 = ("cq", "co")
 
 
 class BF16Weights:
@@ -95,10 +119,15 @@ class BF16Weights:
     FP8_KEYS = {"qkv": None, "o": "self_attn.o", "cq": "cross_attn.q", "co": "cross_attn.o",
                 "1": "ffn.0", "2": "ffn.2"}
 
-    def __init__(self, P, fp8=False, need_bf16=True):
+    def __init__(self, P, fp8=0, need_bf16=True):
         g = P.__getitem__
         C = g("self_attn.q.weight").shape[0]
         dev = g("self_attn.q.weight").device
+        code = int(fp8)
+        keep = {n for i, n in enumerate(PROJ) if (code >> 2) >> i & 1}
+        fp8 = (code & 3) > 0
+        if keep:                 # some projections bf16 beside e4m3 ones: every bf16 copy cast
+            need_bf16 = True
         self.fp8 = fp8
         self.q = {}
         # bf16 path: the six forward projections take their weight TRANSPOSED (self.t[name] =
@@ -140,6 +169,8 @@ class BF16Weights:
         self.w2, self.b2 = cw("ffn.2.weight"), c("ffn.2.bias")
         if fp8:
             for name, pre in self.FP8_KEYS.items():
+                if name in keep:
+                    continue
                 if pre is None:     # q/k/v rows quantised into one [3C, C] operand
                     wq = torch.empty(3 * C, C, dtype=ops.FP8, device=dev)
                     ws = torch.empty(3 * C, dtype=torch.float32, device=dev)
@@ -156,7 +187,7 @@ def lin(W, name, x, **kw):
     path x is quantised per row and the GEMM runs on the block-scaled fp8 MFMA, otherwise bf16."""
     wn = {"qkv": "qkv", "o": "o", "cq": "cq", "co": "co", "1": "1", "2": "2"}[name]
     bias = getattr(W, "b" + wn)
-    if W.fp8:
+    if W.fp8 and name in W.q:
         xq, xs = ops.quant_rows_fp8(x)
         wq, ws = W.q[name]
         return ops.linear_fp8(xq, xs, wq, ws, bias, **kw)
@@ -193,7 +224,7 @@ def block_forward_one(P, W, x, e, ctx, meta, b, save, attn=None, keep_attn=False
                               out_scale=ops.L2Q_SCALE, row0=row0)
     kr, rk = ops.rms_rope_fwd(k_raw, g("self_attn.norm_k.weight"), eps, meta.rope_tab, grid,
                               row0=row0)
-    fwd = ops.attn_fwd_fp8 if meta.fp8 >= 2 else ops.attn_fwd
+    fwd = ops.attn_fwd_fp8 if meta.fp8_mode >= 2 else ops.attn_fwd
     if st is None:
         if attn is not None:
             ao, lse = attn

@@ -55,7 +55,7 @@ def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_h
     kept output / LSE being the head-sharded ones in the same shapes."""
     meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp)
     P = dict(zip(B.param_names(i2v), params))
-    W = B.BF16Weights(P, fp8=fp8 > 0, need_bf16=False)
+    W = B.BF16Weights(P, fp8=fp8, need_bf16=False)
     outs, aos, lses = [], [], []
     for b in range(x.shape[0]):
         o, S = B.block_forward_one(P, W, x[b], e[b], context[b], meta, b, save=False,
@@ -93,7 +93,7 @@ def wan_block_backward(dout: Tensor, x: Tensor, e: Tensor, context: Tensor, para
     meta = _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp)
     names = B.param_names(i2v)
     P = dict(zip(names, params))
-    W = B.BF16Weights(P, fp8=fp8 > 0)
+    W = B.BF16Weights(P, fp8=fp8)
     G = {}
     dxs, des, dcs = [], [], []
     kept = ao.numel() > 0

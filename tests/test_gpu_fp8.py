@@ -162,7 +162,9 @@ def test_block_fp8_vs_fp32_truth():
     scaling cannot lower it.  A broken fp8 kernel (wrong scale, lost k-block) is >= 100 % off,
     > 160x.  The bf16 path itself is also held to the oracle (<= 1e-2).  The same bound holds with
     the C5 self-attention forward (int8 Q.K^T, e4m3 P.V) on as well (block.Meta fp8 = 2):
-    measured within 5 % of the projections-only errors on every tensor (GPU run r3i)."""
+    measured within 5 % of the projections-only errors on every tensor (GPU run r3i).  Round 6:
+    config C5's default keeps the cross-attention q / o projections bf16 (block.C5_KEEP_BF16),
+    which holds the update to SURVEY §8c's absolute 5e-2 as well (2.5 % measured)."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
@@ -181,7 +183,8 @@ def test_block_fp8_vs_fp32_truth():
     e = e0 + P["b.modulation"]
     ctx = torch.randn(1, 512 + 257, C, generator=g).to(torch.bfloat16)
     up = torch.randn(1, L, C, generator=g)
-    hip = {fp8: _block_update(P, names, x, e, ctx, grid, up, i2v, fp8) for fp8 in (0, 1, 2)}
+    c5 = B.fp8_code(2, B.C5_KEEP_BF16)     # config C5's default: cross-attention q / o bf16
+    hip = {fp8: _block_update(P, names, x, e, ctx, grid, up, i2v, fp8) for fp8 in (0, 1, 2, c5)}
 
     def oracle(truth):
         saved = O.bf
@@ -209,6 +212,7 @@ def test_block_fp8_vs_fp32_truth():
         return out
     e16, e8, eor = errs(hip[0], truth), errs(hip[1], truth), errs(ref16, truth)
     e8a = errs(hip[2], truth)
+    e8d = errs(hip[c5], truth)
     e16_vs_oracle = errs(hip[0], ref16)
     print("vs truth: bf16 path", {k: round(v, 4) for k, v in e16.items()})
     print("vs truth: fp8 path ", {k: round(v, 4) for k, v in e8.items()})
@@ -216,10 +220,80 @@ def test_block_fp8_vs_fp32_truth():
     print("vs truth: oracle   ", {k: round(v, 4) for k, v in eor.items()})
     print("fp8 / bf16 ratio   ", {k: round(e8[k] / e16[k], 2) for k in keys})
     print("fp8+attn / bf16    ", {k: round(e8a[k] / e16[k], 2) for k in keys})
+    print("vs truth: C5 default", {k: round(v, 4) for k, v in e8d.items()})
     for k in keys:
         assert e8[k] <= 16 * e16[k] and e8[k] <= 1e-1, (k, e8[k], e16[k])
         assert e8a[k] <= 16 * e16[k] and e8a[k] <= 1e-1, (k, e8a[k], e16[k])
+        assert e8d[k] <= 16 * e16[k] and e8d[k] <= 1e-1, (k, e8d[k], e16[k])
+    # SURVEY §8c's fp8 tolerance, met by the default C5 path (round 6: 2.5 % measured; every
+    # projection on e4m3, the 5.3 % above, does not meet it: test_c5_per_projection_error_table)
+    assert e8d["update"] <= 5e-2 and e8d["dx"] <= 5e-2, e8d
     assert e16_vs_oracle["update"] < 1e-2 and e16_vs_oracle["dx"] < 3e-2, e16_vs_oracle
+
+
+
+
+def test_c5_per_projection_error_table():
+    """which e4m3 operand sets config C5's per-block error?  The real-width I2V
+    block of test_block_fp8_vs_fp32_truth (C = 5120, 40 heads, F = 13 824, 257 + 512 context
+    tokens, L = 4 200), run with e4m3 on ONE forward projection at a time (QKV, self-attn o,
+    cross q, cross o, FFN up, FFN down; every other GEMM bf16), with only the int8 / e4m3
+    self-attention forward, with everything (the C5 path), and with everything but the largest
+    contributor(s) kept bf16 (block.fp8_code); each against the oracle's fp32 truth.  Relative
+    errors add in quadrature (independent roundings), so the table says what keeping a
+    projection bf16 buys.  Asserted: every single-operand error sits between the bf16 path's and
+    the full C5 path's; the table is printed for the record (profiles/r06_c5_projection_table.log)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from shapes import block_shapes, seeded_params
+    from oracle import wan_oracle as O
+    from prfl_amd import block as B
+    torch.set_num_threads(16)
+    C, Fd, nh, i2v = 5120, 13824, 40, True
+    P = seeded_params(block_shapes("b.", C, Fd, i2v), prefix="fp8t.")
+    names = B.param_names(i2v)
+    grid = (3, 35, 40)
+    L = grid[0] * grid[1] * grid[2]
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(1, L, C, generator=g)
+    e0 = torch.randn(1, 6, C, generator=g) * 0.1
+    e = e0 + P["b.modulation"]
+    ctx = torch.randn(1, 512 + 257, C, generator=g).to(torch.bfloat16)
+    up = torch.randn(1, L, C, generator=g)
+    saved = O.bf
+    O.bf = lambda t: t                       # the fp32 truth: every cast point removed
+    try:
+        Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+        xr = x.clone().requires_grad_(True)
+        ref = O.block_forward(Pr, "b.", xr, e0, torch.tensor([grid]), O.rope_freqs(128),
+                              ctx.float(), nh, seq_len=L, i2v=i2v)
+        (ref * up).sum().backward()
+        truth = ((ref - x).detach(), xr.grad)
+    finally:
+        O.bf = saved
+    del Pr, ref
+
+    def err(code):
+        d, gx, _ = _block_update(P, names, x, e, ctx, grid, up, i2v, code)
+        return rel(d, truth[0]), rel(gx, truth[1])
+
+    rows = {"bf16": err(0), "C5 (all e4m3 + attention)": err(B.fp8_code(2))}
+    for pj in B.PROJ:
+        rows[f"only {pj}"] = err(B.fp8_code(1, [q for q in B.PROJ if q != pj]))
+    rows["only attention"] = err(B.fp8_code(2, B.PROJ))
+    singles = sorted(B.PROJ, key=lambda pj: -rows[f"only {pj}"][0])
+    for k in (1, 2):
+        keep = singles[:k]
+        rows[f"C5 with {'+'.join(keep)} bf16"] = err(B.fp8_code(2, keep))
+    print("C5 per-projection error vs the fp32 truth (update, dx):")
+    for k, (u, dx) in rows.items():
+        print(f"  {k:34s} update {u:.4f}  dx {dx:.4f}")
+    quad = (sum(rows[f"only {pj}"][0] ** 2 for pj in B.PROJ) + rows["only attention"][0] ** 2) ** 0.5
+    print(f"  quadrature sum of the singles: update {quad:.4f}")
+    b16, full = rows["bf16"][0], rows["C5 (all e4m3 + attention)"][0]
+    for pj in B.PROJ:
+        assert b16 <= rows[f"only {pj}"][0] <= 1.05 * full, (pj, rows[f"only {pj}"], b16, full)
 
 
 def test_fp8_error_across_a_block_chain():
