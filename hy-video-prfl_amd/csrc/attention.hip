@@ -391,9 +391,40 @@ __device__ __forceinline__ float exp2_poly(float x) {
 }
 #if ATTN_PHASETIME
 __device__ unsigned long long g_attn_phase[8 * 16];
+// the backward kernels' phases: [kernel 0 dK/dV, 1 dQ][wave][16] (slot 15: workgroups)
+__device__ unsigned long long g_attn_bphase[2 * 8 * 16];
 __device__ __forceinline__ unsigned phase_clk() {     // shader cycles (s_memtime, low 32 bits)
   return (unsigned)__builtin_amdgcn_s_memtime();
 }
+// per-wave phase accumulator of the backward kernels (the first 64 workgroups of a launch); each
+// tick is fenced by sched_barrier so the compiler keeps the phase's instructions on its side
+struct BPhase {
+  bool on;
+  unsigned t0, ph[8];
+  __device__ void init(bool o) {
+    on = o;
+    for (int k = 0; k < 8; ++k) ph[k] = 0;
+    __builtin_amdgcn_sched_barrier(0);
+    t0 = phase_clk();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ void tick(int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned t1 = phase_clk();
+    __builtin_amdgcn_sched_barrier(0);
+    ph[k] += t1 - t0;
+    t0 = t1;
+  }
+  __device__ void flush(int kernel, int w, int lane) {
+    if (on && lane == 0) {
+      for (int k = 0; k < 8; ++k) atomicAdd(&g_attn_bphase[(kernel * 8 + w) * 16 + k], (unsigned long long)ph[k]);
+      atomicAdd(&g_attn_bphase[(kernel * 8 + w) * 16 + 15], 1ull);
+    }
+  }
+};
+#define BTICK(k) bp.tick(k)
+#else
+#define BTICK(k)
 #endif
 
 // (Measured and dropped: the O^T accumulators in AGPRs through inline-asm P.V MFMAs -- at two
@@ -1075,6 +1106,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   if (nq > 0) dma_tile(0, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): K fragments, V, tile 0
   __syncthreads();
+#if ATTN_PHASETIME
+  // dK/dV phases: 0 S / dP chain, 1 softmax, 2 DMA issue, 3 pack, 4 dV / dK chain, 5 tile vmcnt,
+  // 6 barrier
+  BPhase bp;
+  bp.init(blockIdx.x < 64);
+#endif
   for (int t = 0; t < nq; ++t) {
     const int st = t & 1;
     if (!ATTN_BWD_DMA_MID && t + 1 < nq) dma_tile(t + 1, st ^ 1);
@@ -1120,6 +1157,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         dpt = mfma32(*(const bf16x8*)(Ds + offB(row, (ks * 2 + hh) * 16)), vfr, dpt);
         if (ks & 1 & ATTN_DKDV_SB) __builtin_amdgcn_sched_barrier(0);
       }
+      BTICK(0);
       // rows q = qb + qt*32 + (r&3) + 8(r>>2) + 4hh
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
@@ -1139,7 +1177,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
             if (qb + q4 + r >= a.Lq) { sacc[rg * 4 + r] = 0.f; dpt[rg * 4 + r] = 0.f; }
         }
       }
+      BTICK(1);
       if (ATTN_BWD_DMA_MID && qt == 0 && t + 1 < nq) dma_tile(t + 1, st ^ 1);
+      BTICK(2);
       bf16x8 pk[2], dk8[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -1150,6 +1190,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
                            f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
                            f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
       }
+      BTICK(3);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
@@ -1163,11 +1204,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         }
         if (ATTN_DKDV_SB & 2) __builtin_amdgcn_sched_barrier(0);
       }
+      BTICK(4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    BTICK(5);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    BTICK(6);
   }
+#if ATTN_PHASETIME
+  bp.flush(0, w, lane);
+#endif
   if (part) {            // unscaled partial dK^T / dV^T of this query share (attn_merge_kv)
     const int64_t r = (int64_t)(blockIdx.x - a.nmain_k) * 256 + w * 32 + l32;
 #pragma unroll
@@ -1323,6 +1370,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
+#if ATTN_PHASETIME
+  // dQ phases: 0 S^T / dP^T chain, 1 softmax, 2 pack, 3 DMA issue, 4 dQ chain, 5 tile vmcnt,
+  // 6 barrier
+  BPhase bp;
+  bp.init(blockIdx.x < 64);
+#endif
   for (int t = 0; t < nkv; ++t) {
     const int kb = (t0 + t) * TK;
     // tile t+1 into the stage tile t-1 used (every wave is past the barrier that ended it);
@@ -1425,6 +1478,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         st = mfma32(*(const bf16x8*)(Ks + offB(row, (ks * 2 + hh) * 16)), qf[ks], st);
         dpt = mfma32(*(const bf16x8*)(Vs + off16(row, ks * 2 + hh)), df[ks], dpt);
       }
+      BTICK(0);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = QS ? __builtin_amdgcn_exp2f(-st[r]) : __builtin_amdgcn_exp2f(st[r] * a.sl2 - lse);
@@ -1435,13 +1489,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         for (int r = 0; r < 16; ++r)
           if (kb + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= a.k_len) dpt[r] = 0.f;
       }
+      BTICK(1);
       bf16x8 dsp[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
         dsp[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
                            f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
                            f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
+      BTICK(2);
       if (ATTN_BWD_DMA_MID && kt == 0 && tn < nkv) dma(tn, stn);
+      BTICK(3);
       // dQ^T += K^T dS^T for this key sub-tile (per dQ tile the same (kt, s2) summation order)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -1454,15 +1511,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
           dq[dt] = mfma32(kf, dsp[s2], dq[dt]);
         }
       }
+      BTICK(4);
     }
     }
     if (!ATTN_DQ_STAGGER && NST == 3 && tn < nkv)   // tile t+1 landed; t+2 may stay in flight
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NKT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    BTICK(5);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    BTICK(6);
   }
+#if ATTN_PHASETIME
+  bp.flush(1, w, lane);
+#endif
   if (ATTN_DQ_STAGGER && !lag) {   // the leaders' extra barrier: the same count on every wave
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2488,5 +2551,11 @@ extern "C" int prfl_attn_phase_read(unsigned long long* host) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_phase), sizeof(unsigned long long) * 128) != hipSuccess) return -1;
   static const unsigned long long zero[128] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+// the backward kernels' [2][8][16] phase cycles (dK/dV, dQ), then cleared
+extern "C" int prfl_attn_bphase_read(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_bphase), sizeof(unsigned long long) * 256) != hipSuccess) return -1;
+  static const unsigned long long zero[256] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_bphase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

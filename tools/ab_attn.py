@@ -45,6 +45,8 @@ def load(path):
     if lib.has_kt:
         lib.prfl_attn_bwd_l2q_kt_ws.argtypes = BWD[:6] + [P] + BWD[6:-2] + [P, I64, P]
         lib.prfl_attn_bwd_l2q_kt_ws.restype = ctypes.c_int
+    if hasattr(lib, "prfl_attn_bphase_read"):
+        lib.prfl_attn_bphase_read.argtypes, lib.prfl_attn_bphase_read.restype = [P], ctypes.c_int
     lib.has_bws = hasattr(lib, "prfl_attn_bwd_ws")
     if lib.has_bws:
         lib.prfl_attn_bwd_ws.argtypes, lib.prfl_attn_bwd_ws.restype = BWD[:-1] + [P, I64, P], ctypes.c_int

@@ -22,6 +22,9 @@ def main():
                     "get q pre-scaled by softmax_scale * log2(e) (rounded to bf16 once)")
     ap.add_argument("--phases", action="store_true", help="libs built with ATTN_PHASETIME=1: after the "
                     "timing, one more forward and the per-wave phase cycles of its first 64 workgroups")
+    ap.add_argument("--bphases", action="store_true", help="libs built with ATTN_PHASETIME=1: after the "
+                    "timing, one more backward and the per-wave phase cycles of the dK/dV and dQ kernels' "
+                    "first 64 workgroups")
     ap.add_argument("--vt", default="", help="comma list of lib indices to run through the VT entry "
                     "(prfl_attn_v_to_vt + prfl_attn_fwd_l2q_vt_ws, the transpose inside the timing)")
     a = ap.parse_args()
@@ -145,6 +148,8 @@ def main():
                     errs[i].append(((o - ref).norm() / ref.norm()).item())
             print("fwd rel-L2 vs fp64 (48 rows x 3 heads): " +
                   " | ".join(f"lib{i} {max(e):.2e}" for i, e in enumerate(errs)), flush=True)
+    if a.bphases:
+        print_bphases(libs, outs, bwd)
     if a.phases:
         import ctypes
         names = ("X (S + P.V MFMAs)", "X vmcnt", "barrier 1", "Y prefetch+tail", "Y vmcnt", "barrier 2",
@@ -163,6 +168,28 @@ def main():
                 print(f"lib{i} wave {wv}: " + ", ".join(f"{names[k]} {buf[wv * 16 + k] / n / 1e3:.1f}k "
                       f"({100 * buf[wv * 16 + k] / max(tot, 1):.1f}%)" for k in range(9))
                       + f" | {n} workgroups", flush=True)
+
+
+def print_bphases(libs, outs, bwd):
+    import ctypes
+    names = {0: ("S/dP chain", "softmax", "DMA issue", "pack", "dV/dK chain", "tile vmcnt", "barrier"),
+             1: ("S/dP chain", "softmax", "pack", "DMA issue", "dQ chain", "tile vmcnt", "barrier")}
+    for i, lib in enumerate(libs):
+        if not hasattr(lib, "prfl_attn_bphase_read"):
+            continue
+        buf = (ctypes.c_ulonglong * 256)()
+        lib.prfl_attn_bphase_read(buf)             # clear
+        bwd(lib, outs[i])
+        torch.cuda.synchronize()
+        assert lib.prfl_attn_bphase_read(buf) == 0
+        for kern, kname in ((0, "dK/dV"), (1, "dQ")):
+            for wv in range(8):
+                base = (kern * 8 + wv) * 16
+                n = max(buf[base + 15], 1)
+                tot = sum(buf[base + k] for k in range(7))
+                print(f"lib{i} {kname} wave {wv}: " + ", ".join(
+                    f"{names[kern][k]} {buf[base + k] / n / 1e3:.1f}k ({100 * buf[base + k] / max(tot, 1):.1f}%)"
+                    for k in range(7)) + f" | total {tot / n / 1e3:.1f}k cycles, {n} workgroups", flush=True)
 
 
 if __name__ == "__main__":
