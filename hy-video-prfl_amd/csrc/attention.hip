@@ -968,6 +968,17 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #ifndef ATTN_BWD_NEGD
 #define ATTN_BWD_NEGD 1
 #endif
+// Backward LDS-DMA issue spread (round 6; phase cycles, profiles/r06_attn_bwd_phases.txt: the
+// next tile's pieces issued as one burst per wave cost the dQ kernel 10-19 % of its wave cycles
+// and dK/dV 5-6 %, all eight waves issuing at the same point of the tile):
+//   ATTN_DQ_DMA_SPLIT 1: dQ's K pieces after key sub-tile 0's pack, its V pieces after sub-tile 1's
+//   ATTN_DKDV_DMA_SPLIT 1: dK/dV's Q (+ LSE / D) pieces after sub-tile 0's softmax, dO after 1's
+#ifndef ATTN_DQ_DMA_SPLIT
+#define ATTN_DQ_DMA_SPLIT 0
+#endif
+#ifndef ATTN_DKDV_DMA_SPLIT
+#define ATTN_DKDV_DMA_SPLIT 0
+#endif
 // dK/dV scheduling fences: bit 0 = one every two k-steps of the S / dP chain, bit 1 = one per
 // dV / dK d-tile (3 = both); 0 / 1 / 2 / 3 tie within 0.3 % (profiles/r04_ab_dkdv_sb.txt)
 #ifndef ATTN_DKDV_SB
@@ -1079,18 +1090,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     t0 = min(share * per, nq);
     nq = min(nq, t0 + per) - t0;
   }
-  auto dma_tile = [&](int t, int st) {     // local tile t = query tile t0 + t
-    char* Qs = smem + V_BYTES + st * STAGE;
+  auto dma_tile = [&](int t, int st, int which = 3) {   // local tile t = query tile t0 + t
+    char* Qs = smem + V_BYTES + st * STAGE;       // which: 1 Q (+ LSE / D), 2 dO, 3 both
     char* Ds = Qs + 16384;
     const int qb = (t0 + t) * 64, rows = min(a.Lq - qb, 64);   // record range < 2^32 bytes
-    const i32x4 sq = make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2));
-    const i32x4 sd = make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2));
+    if (which & 1) {
+      const i32x4 sq = make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2));
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      dma16_buf(sq, voq[i], 0, lds_addr(Qs + (w * 2 + i) * 1024));
-      dma16_buf(sd, vod[i], 0, lds_addr(Ds + (w * 2 + i) * 1024));
+      for (int i = 0; i < 2; ++i) dma16_buf(sq, voq[i], 0, lds_addr(Qs + (w * 2 + i) * 1024));
     }
-    if (w < 2) {   // lane * 4 re-derived here (volatile: not hoisted into a register kept live)
+    if (which & 2) {
+      const i32x4 sd = make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dma16_buf(sd, vod[i], 0, lds_addr(Ds + (w * 2 + i) * 1024));
+    }
+    if ((which & 1) && w < 2) {   // lane * 4 re-derived here (volatile: not hoisted into a register kept live)
       uint32_t l4;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
                    "v_lshlrev_b32 %0, 2, %0" : "=v"(l4));
@@ -1178,7 +1192,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
         }
       }
       BTICK(1);
-      if (ATTN_BWD_DMA_MID && qt == 0 && t + 1 < nq) dma_tile(t + 1, st ^ 1);
+      if (ATTN_BWD_DMA_MID && t + 1 < nq) {
+        if (ATTN_DKDV_DMA_SPLIT) dma_tile(t + 1, st ^ 1, qt == 0 ? 1 : 2);
+        else if (qt == 0) dma_tile(t + 1, st ^ 1);
+      }
       BTICK(2);
       bf16x8 pk[2], dk8[2];
 #pragma unroll
@@ -1325,8 +1342,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   // (the per-lane offsets are re-derived at every tile from a volatile lane id: kept live across
   // the loop they pushed this kernel one VGPR past 256, and the spill's reload + vmcnt(0) sat in
   // front of every tile's DMA issue)
-  auto dma = [&](int tl, int st) {     // local tile tl = key tile t0 + tl
-    char* Ks = smem + st * SB;
+  auto dma = [&](int tl, int st, int which = 3) {   // local tile tl = key tile t0 + tl
+    char* Ks = smem + st * SB;                      // which: 1 K, 2 V, 3 both
     char* Vs = Ks + SV;
     const int t = t0 + tl;
     const int rows = min(a.Lk - t * TK, TK);
@@ -1338,10 +1355,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     for (int i = 0; i < NKT; ++i) {
       const int row = (w * NKT + i) * 4 + (ln >> 4), pc = ln & 15;
       const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      dma16_buf(sk, (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4), 0,
-                lds_addr(Ks + (w * NKT + i) * 1024));
-      dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4), 0,
-                lds_addr(Vs + (w * NKT + i) * 1024));
+      if (which & 1)
+        dma16_buf(sk, (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4), 0,
+                  lds_addr(Ks + (w * NKT + i) * 1024));
+      if (which & 2)
+        dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4), 0,
+                  lds_addr(Vs + (w * NKT + i) * 1024));
     }
     if (KT) {          // K^T tile: one contiguous 24 KiB run, lane-linear pieces
       const i32x4 skt = make_srd(KTb + (int64_t)t * TK * HD, (uint32_t)SV);
@@ -1497,7 +1516,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
                            f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
                            f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
       BTICK(2);
-      if (ATTN_BWD_DMA_MID && kt == 0 && tn < nkv) dma(tn, stn);
+      if (ATTN_BWD_DMA_MID && tn < nkv) {
+        if (ATTN_DQ_DMA_SPLIT && NST == 2 && !KT) {
+          if (kt < 2) dma(tn, stn, kt == 0 ? 1 : 2);
+        } else if (kt == 0) {
+          dma(tn, stn);
+        }
+      }
       BTICK(3);
       // dQ^T += K^T dS^T for this key sub-tile (per dQ tile the same (kt, s2) summation order)
 #pragma unroll

@@ -435,6 +435,239 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_wave_kernel(
     *(f32x4*)(part0 + (int64_t)blockIdx.x * C + c * 4) = acc[c];
 }
 
+// ---- RMSNorm + RoPE, column-fixed (round 6, RMS_COLS) -----------------------------------------
+// Thread t of a C/16-thread workgroup owns columns [8t, 8t + 8) and [8(t + C/16), +8) of EVERY row:
+// its 16 w values and its 4 RoPE pair indices are loaded once, and a workgroup streams a block of
+// RC_ROWS rows RC_R at a time (2 x 16-B loads per thread per row, RC_R rows in flight), the rows'
+// sums of squares reduced across the workgroup through LDS with one barrier per RC_R rows
+// (double-buffered partial array).  The backward keeps its 16 d w partial sums in registers across
+// the block of rows and holds each row's dout / x between its two passes.  Same per-element
+// arithmetic as the kernels above; the sum of squares of a row is added in another order.
+#ifndef RMS_COLS
+#define RMS_COLS 1
+#endif
+constexpr int RC_R = 4;             // rows in flight per workgroup (forward)
+constexpr int RC_RB = 2;            // (backward: two operands held per row)
+constexpr int RC_ROWS = 32;         // rows per workgroup (= prfl_norm_rows_per_part for the partial rows)
+constexpr int RC_MAXT = 512;        // C <= 8192
+
+template <bool BWD>
+__device__ __forceinline__ void rc_cols(int C, int& nt, int& t, bool& act) {
+  nt = C / 16;
+  t = threadIdx.x;
+  act = t < nt;
+}
+
+__global__ __launch_bounds__(RC_MAXT) void rms_rope_fwd_cols_kernel(
+    const bf16* __restrict__ x, int64_t ldx, int L, int C, const float* __restrict__ w, float eps,
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ out,
+    int64_t ldo, float* __restrict__ rstd_out, float oscale) {
+  __shared__ float red[2][RC_R][RC_MAXT / 64];
+  int nt, t;
+  bool act;
+  rc_cols<false>(C, nt, t, act);
+  const int nw = (blockDim.x + 63) >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = t * 8, c1 = (t + nt) * 8;           // element offsets of the two chunks
+  const int pair0 = (c0 & 127) >> 1;                  // == (c1 & 127) >> 1: C / 16 * 8 = C / 2 % 128 == 0
+  float wr[16];
+  if (act) {
+    const f32x4 a0 = ldf4(w, c0), a1 = ldf4(w, c0 + 4), b0 = ldf4(w, c1), b1 = ldf4(w, c1 + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      wr[r] = a0[r];
+      wr[4 + r] = a1[r];
+      wr[8 + r] = b0[r];
+      wr[12 + r] = b1[r];
+    }
+  }
+  const int64_t rb = (int64_t)blockIdx.x * RC_ROWS;
+  for (int it = 0; it < RC_ROWS / RC_R; ++it) {
+    const int buf = it & 1;
+    bf16x8 v[RC_R][2];
+    float ss[RC_R];
+#pragma unroll
+    for (int j = 0; j < RC_R; ++j) {
+      const int64_t row = rb + it * RC_R + j;
+      ss[j] = 0.f;
+      if (act && row < L) {
+        v[j][0] = *(const bf16x8*)(x + row * ldx + c0);
+        v[j][1] = *(const bf16x8*)(x + row * ldx + c1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) ss[j] += bf2f(v[j][h][r]) * bf2f(v[j][h][r]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RC_R; ++j) {
+      const float sw = wave_sum(ss[j]);
+      if (lane == 0) red[buf][j][wv] = sw;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RC_R; ++j) {
+      const int64_t row = rb + it * RC_R + j;
+      if (row >= L) break;
+      float tot = 0.f;
+      for (int k = 0; k < nw; ++k) tot += red[buf][j][k];
+      const float rstd = rsqrtf(tot / C + eps);
+      if (threadIdx.x == 0) rstd_out[row] = rstd;
+      if (!act) continue;
+      int pf, ph, pw;
+      bool rot;
+      rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
+      rot = rot && tab != nullptr;
+      float2 cs[4];
+      if (rot) rope_cs4(tab, pair0, pf, ph, pw, cs);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float y[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) y[r] = mul_rn(bfr(bf2f(v[j][h][r]) * rstd), wr[8 * h + r]);
+        bf16x8 o;
+        if (rot) {
+#pragma unroll
+          for (int pp = 0; pp < 4; ++pp) {
+            const float a = y[2 * pp], bq = y[2 * pp + 1];
+            o[2 * pp] = f2bf(__fmul_rn(__fsub_rn(__fmul_rn(a, cs[pp].x), __fmul_rn(bq, cs[pp].y)), oscale));
+            o[2 * pp + 1] = f2bf(__fmul_rn(__fadd_rn(__fmul_rn(a, cs[pp].y), __fmul_rn(bq, cs[pp].x)), oscale));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = f2bf(__fmul_rn(y[r], oscale));
+        }
+        *(bf16x8*)(out + row * ldo + (h ? c1 : c0)) = o;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(RC_MAXT) void rms_rope_bwd_cols_kernel(
+    const bf16* __restrict__ dout, int64_t lddo, const bf16* __restrict__ x, int64_t ldx,
+    const float* __restrict__ rstd_in, int L, int C, const float* __restrict__ w,
+    const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ dx,
+    int64_t lddx, float* __restrict__ part0, float oscale) {
+  __shared__ float red[2][RC_RB][RC_MAXT / 64];
+  int nt, t;
+  bool act;
+  rc_cols<true>(C, nt, t, act);
+  const int nw = (blockDim.x + 63) >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = t * 8, c1 = (t + nt) * 8;
+  const int pair0 = (c0 & 127) >> 1;
+  float wr[16], p0[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p0[r] = 0.f;
+  if (act) {
+    const f32x4 a0 = ldf4(w, c0), a1 = ldf4(w, c0 + 4), b0 = ldf4(w, c1), b1 = ldf4(w, c1 + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      wr[r] = a0[r];
+      wr[4 + r] = a1[r];
+      wr[8 + r] = b0[r];
+      wr[12 + r] = b1[r];
+    }
+  }
+  // dy = the conj-rotated (dout * oscale) of one 8-element chunk
+  auto rot8 = [&](const bf16x8& gq, bool rot, const float2 (&cs)[4], float (&g8)[8]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) g8[r] = bf2f(gq[r]) * oscale;
+    if (rot) {
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp) {
+        const float ga = g8[2 * pp], gb = g8[2 * pp + 1];
+        g8[2 * pp] = ga * cs[pp].x + gb * cs[pp].y;
+        g8[2 * pp + 1] = gb * cs[pp].x - ga * cs[pp].y;
+      }
+    }
+  };
+  const int64_t rb = (int64_t)blockIdx.x * RC_ROWS;
+  for (int it = 0; it < RC_ROWS / RC_RB; ++it) {
+    const int buf = it & 1;
+    bf16x8 gv[RC_RB][2], xv[RC_RB][2];     // the rows held (bf16) between the two passes
+    float sp[RC_RB];
+#pragma unroll
+    for (int j = 0; j < RC_RB; ++j) {
+      const int64_t row = rb + it * RC_RB + j;
+      sp[j] = 0.f;
+      if (act && row < L) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          gv[j][h] = *(const bf16x8*)(dout + row * lddo + (h ? c1 : c0));
+          xv[j][h] = *(const bf16x8*)(x + row * ldx + (h ? c1 : c0));
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RC_RB; ++j) {
+      const int64_t row = rb + it * RC_RB + j;
+      if (act && row < L) {
+        const float rstd = rstd_in[row];
+        int pf, ph, pw;
+        bool rot;
+        rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
+        rot = rot && tab != nullptr;
+        float2 cs[4];
+        if (rot) rope_cs4(tab, pair0, pf, ph, pw, cs);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float g8[8];
+          rot8(gv[j][h], rot, cs, g8);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int e = 8 * h + r;
+            const float xhat = bf2f(xv[j][h][r]) * rstd;
+            const float d = bfr(g8[r] * wr[e]);
+            p0[e] += g8[r] * bfr(xhat);
+            sp[j] += d * xhat;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RC_RB; ++j) {
+      const float sw = wave_sum(sp[j]);
+      if (lane == 0) red[buf][j][wv] = sw;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RC_RB; ++j) {
+      const int64_t row = rb + it * RC_RB + j;
+      if (!act || row >= L) continue;
+      float tot = 0.f;
+      for (int k = 0; k < nw; ++k) tot += red[buf][j][k];
+      const float m = tot / C;
+      const float rstd = rstd_in[row];
+      int pf, ph, pw;
+      bool rot;
+      rope_pos(row0 + row, F, Hg, Wg, pf, ph, pw, rot);
+      rot = rot && tab != nullptr;
+      float2 cs[4];
+      if (rot) rope_cs4(tab, pair0, pf, ph, pw, cs);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float g8[8];
+        rot8(gv[j][h], rot, cs, g8);
+        bf16x8 o;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int e = 8 * h + r;
+          const float xhat = bf2f(xv[j][h][r]) * rstd;
+          const float d = bfr(g8[r] * wr[e]);
+          o[r] = f2bf(rstd * (d - xhat * m));
+        }
+        *(bf16x8*)(dx + row * lddx + (h ? c1 : c0)) = o;
+      }
+    }
+  }
+  if (act) {
+    float* pr = part0 + (int64_t)blockIdx.x * C;
+    *(f32x4*)(pr + c0) = (f32x4){p0[0], p0[1], p0[2], p0[3]};
+    *(f32x4*)(pr + c0 + 4) = (f32x4){p0[4], p0[5], p0[6], p0[7]};
+    *(f32x4*)(pr + c1) = (f32x4){p0[8], p0[9], p0[10], p0[11]};
+    *(f32x4*)(pr + c1 + 4) = (f32x4){p0[12], p0[13], p0[14], p0[15]};
+  }
+}
+
 // LN + modulate forward: one wave per row, the row (C <= 5120 -> 20 float4 chunks per lane) held
 // in registers, both reductions wave shuffles (two-pass mean / variance); the per-column
 // coefficients — (1 + scale, shift) or (w, b) — are staged once per workgroup in LDS and each wave
@@ -513,8 +746,254 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
   }
 }
 
+// ---- LN + modulate, column-fixed (round 6, LN_COLS) --------------------------------------------
+// The layout of the column-fixed RMSNorm kernels: thread t of a C/16-thread workgroup owns columns
+// [8t, 8t + 8) and [8(t + C/16), +8) of every row, its 16 (1 + scale | w) and (shift | b)
+// coefficients in registers (no LDS staging), a block of LC_ROWS rows streamed LC_R at a time; the
+// forward's two-pass mean / variance takes two cross-wave reductions per LC_R rows, the
+// backward's two column sums (d scale | d w, d shift | d b) stay in registers over the block and
+// its two row sums share one reduction.  Same per-element arithmetic as ln_mod_fwd_lds_kernel /
+// ln_mod_bwd_kernel; the row sums add in another order.
+#ifndef LN_COLS
+#define LN_COLS 1
+#endif
+constexpr int LC_R = 4;             // rows in flight (forward)
+constexpr int LC_RB = 2;            // rows in flight (backward)
+
+template <int N>
+__device__ __forceinline__ void ld_cols(const void* p, int64_t off, int x_bf16, float (&v)[N]) {
+  static_assert(N == 8, "8-element chunk");
+  if (x_bf16) {
+    const bf16x8 q = *(const bf16x8*)((const bf16*)p + off);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = bf2f(q[r]);
+  } else {
+    const f32x4 a = *(const f32x4*)((const float*)p + off), b = *(const f32x4*)((const float*)p + off + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = a[r];
+      v[r + 4] = b[r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(RC_MAXT) void ln_mod_fwd_cols_kernel(
+    const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ w,
+    const float* __restrict__ b, float eps, bf16* __restrict__ out, int64_t ldo,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  __shared__ float red[2][2][LC_R][RC_MAXT / 64];
+  const int nt = C / 16, t = threadIdx.x;
+  const bool act = t < nt;
+  const int nw = (blockDim.x + 63) >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = t * 8, c1 = (t + nt) * 8;
+  float ca[16], cb[16];
+  if (act) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = h ? c1 : c0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 A = w ? ldf4(w, c + 4 * q) : ldf4(scale, c + 4 * q);
+        const f32x4 Bv = w ? (b ? ldf4(b, c + 4 * q) : (f32x4){0, 0, 0, 0}) : ldf4(shift, c + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ca[8 * h + 4 * q + r] = w ? A[r] : 1.f + A[r];
+          cb[8 * h + 4 * q + r] = Bv[r];
+        }
+      }
+    }
+  }
+  const int64_t rb = (int64_t)blockIdx.x * RC_ROWS;
+  for (int it = 0; it < RC_ROWS / LC_R; ++it) {
+    const int buf = it & 1;
+    float v[LC_R][16], ps[LC_R];
+#pragma unroll
+    for (int j = 0; j < LC_R; ++j) {
+      const int64_t row = rb + it * LC_R + j;
+      ps[j] = 0.f;
+      if (act && row < L) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float q8[8];
+          ld_cols(x, row * ldx + (h ? c1 : c0), x_bf16, q8);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            v[j][8 * h + r] = q8[r];
+            ps[j] += q8[r];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LC_R; ++j) {
+      const float sw = wave_sum(ps[j]);
+      if (lane == 0) red[buf][0][j][wv] = sw;
+    }
+    __syncthreads();
+    float mean[LC_R];
+#pragma unroll
+    for (int j = 0; j < LC_R; ++j) {
+      float tot = 0.f;
+      for (int k = 0; k < nw; ++k) tot += red[buf][0][j][k];
+      mean[j] = tot / C;
+      float sq = 0.f;
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float d = v[j][e] - mean[j];
+          sq += d * d;
+        }
+      }
+      const float sw = wave_sum(sq);
+      if (lane == 0) red[buf][1][j][wv] = sw;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < LC_R; ++j) {
+      const int64_t row = rb + it * LC_R + j;
+      if (row >= L) break;
+      float tot = 0.f;
+      for (int k = 0; k < nw; ++k) tot += red[buf][1][j][k];
+      const float rstd = rsqrtf(tot / C + eps);
+      if (threadIdx.x == 0) {
+        mean_out[row] = mean[j];
+        rstd_out[row] = rstd;
+      }
+      if (!act) continue;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 o;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int e = 8 * h + r;
+          float xh = (v[j][e] - mean[j]) * rstd;
+          if (!w && x_bf16) xh = bfr(xh);  // WanLayerNorm.type_as(x) for a bf16 input
+          o[r] = f2bf(mul_rn(xh, ca[e]) + cb[e]);
+        }
+        *(bf16x8*)(out + row * ldo + (h ? c1 : c0)) = o;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(RC_MAXT) void ln_mod_bwd_cols_kernel(
+    const bf16* __restrict__ dy, int64_t lddy, const void* __restrict__ x, int x_bf16, int64_t ldx,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int L, int C,
+    const float* __restrict__ scale, const float* __restrict__ w, float* __restrict__ dx,
+    int64_t lddx, int dx_accumulate, float* __restrict__ part0, float* __restrict__ part1) {
+  __shared__ float red[2][2][LC_RB][RC_MAXT / 64];
+  const int nt = C / 16, t = threadIdx.x;
+  const bool act = t < nt;
+  const int nw = (blockDim.x + 63) >> 6, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = t * 8, c1 = (t + nt) * 8;
+  float m[16], p0[16], p1[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) p0[e] = p1[e] = 0.f;
+  if (act) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 A = w ? ldf4(w, (h ? c1 : c0) + 4 * q) : ldf4(scale, (h ? c1 : c0) + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m[8 * h + 4 * q + r] = w ? A[r] : 1.f + A[r];
+      }
+  }
+  const int64_t rb = (int64_t)blockIdx.x * RC_ROWS;
+  for (int it = 0; it < RC_ROWS / LC_RB; ++it) {
+    const int buf = it & 1;
+    bf16x8 dv[LC_RB][2];                  // (x is re-read in the second pass: L1 / L2)
+    float s1[LC_RB], s2[LC_RB];
+#pragma unroll
+    for (int j = 0; j < LC_RB; ++j) {
+      const int64_t row = rb + it * LC_RB + j;
+      s1[j] = s2[j] = 0.f;
+      if (act && row < L) {
+        const float mean = mean_in[row], rstd = rstd_in[row];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float q8[8];
+          ld_cols(x, row * ldx + (h ? c1 : c0), x_bf16, q8);
+          dv[j][h] = *(const bf16x8*)(dy + row * lddy + (h ? c1 : c0));
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int e = 8 * h + r;
+            const float xhat = (q8[r] - mean) * rstd;
+            const float d = bf2f(dv[j][h][r]);
+            const float xu = (!w && x_bf16) ? bfr(xhat) : xhat;
+            p0[e] += d * xu;
+            p1[e] += d;
+            const float gg = d * m[e];
+            s1[j] += gg;
+            s2[j] += gg * xhat;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LC_RB; ++j) {
+      const float a = wave_sum(s1[j]), c = wave_sum(s2[j]);
+      if (lane == 0) {
+        red[buf][0][j][wv] = a;
+        red[buf][1][j][wv] = c;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < LC_RB; ++j) {
+      const int64_t row = rb + it * LC_RB + j;
+      if (!act || row >= L) continue;
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = 0; k < nw; ++k) {
+        t1 += red[buf][0][j][k];
+        t2 += red[buf][1][j][k];
+      }
+      const float m1 = t1 / C, m2 = t2 / C;
+      const float mean = mean_in[row], rstd = rstd_in[row];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float* dp = dx + row * lddx + (h ? c1 : c0);
+        float q8[8];
+        ld_cols(x, row * ldx + (h ? c1 : c0), x_bf16, q8);
+        f32x4 o[2];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int e = 8 * h + r;
+          const float xhat = (q8[r] - mean) * rstd;
+          const float gg = bf2f(dv[j][h][r]) * m[e];
+          o[r >> 2][r & 3] = rstd * (gg - m1 - xhat * m2);
+        }
+        if (dx_accumulate) {
+          o[0] = o[0] + *(const f32x4*)dp;
+          o[1] = o[1] + *(const f32x4*)(dp + 4);
+        }
+        *(f32x4*)dp = o[0];
+        *(f32x4*)(dp + 4) = o[1];
+      }
+    }
+  }
+  if (act) {
+    float* q0 = part0 + (int64_t)blockIdx.x * C;
+    float* q1 = part1 + (int64_t)blockIdx.x * C;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = h ? c1 : c0;
+      *(f32x4*)(q0 + c) = (f32x4){p0[8 * h], p0[8 * h + 1], p0[8 * h + 2], p0[8 * h + 3]};
+      *(f32x4*)(q0 + c + 4) = (f32x4){p0[8 * h + 4], p0[8 * h + 5], p0[8 * h + 6], p0[8 * h + 7]};
+      *(f32x4*)(q1 + c) = (f32x4){p1[8 * h], p1[8 * h + 1], p1[8 * h + 2], p1[8 * h + 3]};
+      *(f32x4*)(q1 + c + 4) = (f32x4){p1[8 * h + 4], p1[8 * h + 5], p1[8 * h + 6], p1[8 * h + 7]};
+    }
+  }
+}
+
 constexpr int BWD_ROWS = 32;
 bool bad_c(int64_t C) { return C <= 0 || (C % 4) != 0 || C > 4 * MAXV * NT; }
+// the column-fixed RMSNorm+RoPE kernels: C / 16 threads, two 16-B chunks per thread per row
+bool cols_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int64_t C) {
+  return C % 256 == 0 && C / 16 <= RC_MAXT && lda % 8 == 0 && ldb % 8 == 0 &&
+         ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
+}
 // the one-wave-per-row RMSNorm+RoPE kernels: 16-B chunks of both row-major operands
 bool wave_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int64_t C) {
   return C % 8 == 0 && C <= 64 * RW_NJ * 8 && lda % 8 == 0 && ldb % 8 == 0 &&
@@ -532,9 +1011,15 @@ extern "C" int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L
   if (bad_c(C) || (!w && (!scale || !shift))) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  hipLaunchKernelGGL(ln_mod_fwd_lds_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
-                     dim3(NT), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps,
-                     (bf16*)out, ldo, mean, rstd);
+  if (LN_COLS && cols_ok(x, ldx * (x_bf16 ? 1 : 2), out, ldo, C)) {
+    hipLaunchKernelGGL(ln_mod_fwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
+                       dim3(((C / 16) + 63) / 64 * 64), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale,
+                       shift, w, b, eps, (bf16*)out, ldo, mean, rstd);
+  } else {
+    hipLaunchKernelGGL(ln_mod_fwd_lds_kernel, dim3((L + NT / 64 * RPW - 1) / (NT / 64 * RPW)),
+                       dim3(NT), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale, shift, w, b, eps,
+                       (bf16*)out, ldo, mean, rstd);
+  }
   prfl_prof::set_work((double)L * C * ((x_bf16 ? 2 : 4) + 2));
   prfl_prof::end(KID_LN, s);
   PRFL_LAUNCH_CHECK();
@@ -550,9 +1035,15 @@ extern "C" int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int 
   if (bad_c(C) || (!w && !scale)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  hipLaunchKernelGGL(ln_mod_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
-                     0, s, (const bf16*)dy, lddy, x, x_bf16, ldx, mean, rstd, (int)L, (int)C, scale,
-                     w, dx, lddx, dx_accumulate, part0, part1);
+  if (LN_COLS && cols_ok(x, ldx * (x_bf16 ? 1 : 2), dy, lddy, C) && cols_ok(dx, lddx * 2, dx, lddx * 2, C)) {
+    hipLaunchKernelGGL(ln_mod_bwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
+                       dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)dy, lddy, x, x_bf16, ldx,
+                       mean, rstd, (int)L, (int)C, scale, w, dx, lddx, dx_accumulate, part0, part1);
+  } else {
+    hipLaunchKernelGGL(ln_mod_bwd_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS), dim3(NT),
+                       0, s, (const bf16*)dy, lddy, x, x_bf16, ldx, mean, rstd, (int)L, (int)C, scale,
+                       w, dx, lddx, dx_accumulate, part0, part1);
+  }
   prfl_prof::set_work((double)L * C * (2 + (x_bf16 ? 2 : 4) + 4 + (dx_accumulate ? 4 : 0)));
   prfl_prof::end(KID_LN, s);
   PRFL_LAUNCH_CHECK();
@@ -570,7 +1061,12 @@ extern "C" int prfl_rms_rope_fwd_pos(const void* x, int64_t ldx, int64_t L, int6
   // (round 3: a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p,
   // profiles/r03_ab_rms_rope_wave.txt; round 6's RMS_WAVE form adds 16-B chunks, w in LDS and
   // several rows per wave: profiles/r06_ab_norms.txt)
-  if (RMS_WAVE && wave_ok(x, ldx, out, ldo, C)) {
+  if (RMS_COLS && cols_ok(x, ldx, out, ldo, C)) {
+    hipLaunchKernelGGL(rms_rope_fwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
+                       dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)x, ldx, (int)L, (int)C, w,
+                       eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)out, ldo,
+                       rstd, out_scale);
+  } else if (RMS_WAVE && wave_ok(x, ldx, out, ldo, C)) {
     const int64_t rows = NT / 64 * RW_RPW;
     hipLaunchKernelGGL(rms_rope_fwd_wave_kernel, dim3((L + rows - 1) / rows), dim3(NT), 0, s,
                        (const bf16*)x, ldx, (int)L, (int)C, w, eps, (const float2*)rope_tab, (int)F,
@@ -595,7 +1091,13 @@ extern "C" int prfl_rms_rope_bwd_pos(const void* dout, int64_t lddo, const void*
   if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
-  if (RMS_WAVE && wave_ok(x, ldx, dx, lddx, C) && wave_ok(dout, lddo, dout, lddo, C)) {
+  if (RMS_COLS && cols_ok(x, ldx, dx, lddx, C) && cols_ok(dout, lddo, dout, lddo, C)) {
+    static_assert(RC_ROWS == BWD_ROWS, "one partial row per prfl_norm_rows_per_part rows");
+    hipLaunchKernelGGL(rms_rope_bwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
+                       dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)dout, lddo, (const bf16*)x,
+                       ldx, rstd, (int)L, (int)C, w, (const float2*)rope_tab, (int)F, (int)Hg,
+                       (int)Wg, row0, (bf16*)dx, lddx, part0, out_scale);
+  } else if (RMS_WAVE && wave_ok(x, ldx, dx, lddx, C) && wave_ok(dout, lddo, dout, lddo, C)) {
     hipLaunchKernelGGL(rms_rope_bwd_wave_kernel<BWD_ROWS>, dim3((L + BWD_ROWS - 1) / BWD_ROWS),
                        dim3(NT), 0, s, (const bf16*)dout, lddo, (const bf16*)x, ldx, rstd, (int)L,
                        (int)C, w, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0,

@@ -5,6 +5,8 @@ At the 720p shapes of the fused block (L = 73 920, C = 5120):
            (bytes: read 2 + write 2 per element)
   rms_bwd  prfl_rms_rope_bwd_pos of the same (read dout 2 + x 2, write dx 2; the d w partial rows)
   ln_fwd   prfl_ln_mod_fwd on the fp32 residual stream with (scale, shift) (read 4 + write 2)
+  ln_bwd   prfl_ln_mod_bwd of the same, accumulating into an fp32 dx (read dy 2 + x 4 + dx 4, write
+           dx 4, accumulated over the repetitions; the two partial column-sum rows)
 HIP events on the launch stream; prints medians, GB/s and the largest output difference vs the
 first build (bf16 ulps; rstd / partial sums relative)."""
 import argparse
@@ -23,6 +25,7 @@ SIGS = {
     "prfl_rms_rope_fwd_pos": [P, I64, I64, I64, P, F32, P, I64, I64, I64, I64, P, I64, P, F32, P],
     "prfl_rms_rope_bwd_pos": [P, I64, P, I64, P, I64, I64, P, P, I64, I64, I64, I64, P, I64, P, F32, P],
     "prfl_ln_mod_fwd": [P, I32, I64, I64, I64, P, P, P, P, F32, P, I64, P, P, P],
+    "prfl_ln_mod_bwd": [P, I64, P, I32, I64, P, P, I64, I64, P, P, P, I64, I32, P, P, P],
 }
 
 
@@ -63,6 +66,10 @@ def main():
     o_ln = [torch.empty(L, C, device=dev, dtype=torch.bfloat16) for _ in libs]
     mean_ln = [torch.empty(L, device=dev) for _ in libs]
     rstd_ln = [torch.empty(L, device=dev) for _ in libs]
+    dyl = torch.randn(L, C, device=dev, generator=g).to(torch.bfloat16)
+    dxl = [torch.zeros(L, C, device=dev) for _ in libs]
+    p0l = [torch.empty((L + 31) // 32, C, device=dev) for _ in libs]
+    p1l = [torch.empty((L + 31) // 32, C, device=dev) for _ in libs]
     st = torch.cuda.current_stream().cuda_stream
     osc = 1.4426950408889634 / math.sqrt(128)
 
@@ -75,11 +82,15 @@ def main():
             return lib.prfl_rms_rope_bwd_pos(dq.data_ptr(), C, qkv.data_ptr(), 3 * C, rstd[0].data_ptr(), L, C,
                                              w.data_ptr(), tab.data_ptr(), F, Hg, Wg, 0, o_rb[i].data_ptr(), C,
                                              part[i].data_ptr(), osc, st)
-        return lib.prfl_ln_mod_fwd(xres.data_ptr(), 0, C, L, C, sc_.data_ptr(), sh_.data_ptr(), None, None,
-                                   1e-6, o_ln[i].data_ptr(), C, mean_ln[i].data_ptr(), rstd_ln[i].data_ptr(), st)
+        if which == "ln_fwd":
+            return lib.prfl_ln_mod_fwd(xres.data_ptr(), 0, C, L, C, sc_.data_ptr(), sh_.data_ptr(), None, None,
+                                       1e-6, o_ln[i].data_ptr(), C, mean_ln[i].data_ptr(), rstd_ln[i].data_ptr(), st)
+        return lib.prfl_ln_mod_bwd(dyl.data_ptr(), C, xres.data_ptr(), 0, C, mean_ln[0].data_ptr(),
+                                   rstd_ln[0].data_ptr(), L, C, sc_.data_ptr(), None, dxl[i].data_ptr(), C, 1,
+                                   p0l[i].data_ptr(), p1l[i].data_ptr(), st)
 
-    byts = {"rms_fwd": L * C * 4, "rms_bwd": L * C * 6, "ln_fwd": L * C * 6}
-    for which in ("rms_fwd", "rms_bwd", "ln_fwd"):
+    byts = {"rms_fwd": L * C * 4, "rms_bwd": L * C * 6, "ln_fwd": L * C * 6, "ln_bwd": L * C * 14}
+    for which in ("rms_fwd", "rms_bwd", "ln_fwd", "ln_bwd"):
         ts = [[] for _ in libs]
         for r in range(a.reps + 1):
             for i in range(n):
@@ -98,8 +109,11 @@ def main():
         elif which == "rms_bwd":
             diff = [f"{ulps(o_rb[i], o_rb[0])} ulp, dw {((part[i].sum(0) - part[0].sum(0)).norm() / part[0].sum(0).norm()).item():.1e}"
                     for i in range(n)]
-        else:
+        elif which == "ln_fwd":
             diff = [f"{ulps(o_ln[i], o_ln[0])} ulp" for i in range(n)]
+        else:
+            diff = [f"dx {((dxl[i] - dxl[0]).norm() / dxl[0].norm()).item():.1e}, d scale "
+                    f"{((p0l[i].sum(0) - p0l[0].sum(0)).norm() / p0l[0].sum(0).norm()).item():.1e}" for i in range(n)]
         print(f"{which} 720p: " + " | ".join(
             f"lib{i} {m:.3f} ms {byts[which] / m / 1e6:.0f} GB/s ({dd})" for i, (m, dd) in enumerate(zip(meds, diff))),
             flush=True)
