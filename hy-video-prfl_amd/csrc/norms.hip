@@ -444,8 +444,9 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_wave_kernel(
 // the block of rows and holds each row's dout / x between its two passes.  Same per-element
 // arithmetic as the kernels above; the sum of squares of a row is added in another order.
 #ifndef RMS_COLS
-#define RMS_COLS 1
-#endif
+#define RMS_COLS 2          // bit 0: forward, bit 1: backward (profiles/r06_ab_norms_cols.txt: the
+#endif                      // forward runs 0.41 ms here vs 0.33 ms one-wave-per-row, 0.50 ms with
+                            // the next rows prefetched before the barrier)
 constexpr int RC_R = 4;             // rows in flight per workgroup (forward)
 constexpr int RC_RB = 2;            // (backward: two operands held per row)
 constexpr int RC_ROWS = 32;         // rows per workgroup (= prfl_norm_rows_per_part for the partial rows)
@@ -755,8 +756,8 @@ __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
 // its two row sums share one reduction.  Same per-element arithmetic as ln_mod_fwd_lds_kernel /
 // ln_mod_bwd_kernel; the row sums add in another order.
 #ifndef LN_COLS
-#define LN_COLS 1
-#endif
+#define LN_COLS 2           // bit 0: forward, bit 1: backward (forward 0.51 ms vs 0.46-0.49 ms for
+#endif                      // ln_mod_fwd_lds_kernel; backward 1.13-1.15 ms either way)
 constexpr int LC_R = 4;             // rows in flight (forward)
 constexpr int LC_RB = 2;            // rows in flight (backward)
 
@@ -1011,7 +1012,7 @@ extern "C" int prfl_ln_mod_fwd(const void* x, int x_bf16, int64_t ldx, int64_t L
   if (bad_c(C) || (!w && (!scale || !shift))) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  if (LN_COLS && cols_ok(x, ldx * (x_bf16 ? 1 : 2), out, ldo, C)) {
+  if ((LN_COLS & 1) && cols_ok(x, ldx * (x_bf16 ? 1 : 2), out, ldo, C)) {
     hipLaunchKernelGGL(ln_mod_fwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
                        dim3(((C / 16) + 63) / 64 * 64), 0, s, x, x_bf16, ldx, (int)L, (int)C, scale,
                        shift, w, b, eps, (bf16*)out, ldo, mean, rstd);
@@ -1035,7 +1036,7 @@ extern "C" int prfl_ln_mod_bwd(const void* dy, int64_t lddy, const void* x, int 
   if (bad_c(C) || (!w && !scale)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_LN, s);
-  if (LN_COLS && cols_ok(x, ldx * (x_bf16 ? 1 : 2), dy, lddy, C) && cols_ok(dx, lddx * 2, dx, lddx * 2, C)) {
+  if ((LN_COLS & 2) && cols_ok(x, ldx * (x_bf16 ? 1 : 2), dy, lddy, C) && cols_ok(dx, lddx * 2, dx, lddx * 2, C)) {
     hipLaunchKernelGGL(ln_mod_bwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
                        dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)dy, lddy, x, x_bf16, ldx,
                        mean, rstd, (int)L, (int)C, scale, w, dx, lddx, dx_accumulate, part0, part1);
@@ -1061,7 +1062,7 @@ extern "C" int prfl_rms_rope_fwd_pos(const void* x, int64_t ldx, int64_t L, int6
   // (round 3: a one-wave-per-row form with the table loads hoisted ran 0.545 vs 0.456 ms at 720p,
   // profiles/r03_ab_rms_rope_wave.txt; round 6's RMS_WAVE form adds 16-B chunks, w in LDS and
   // several rows per wave: profiles/r06_ab_norms.txt)
-  if (RMS_COLS && cols_ok(x, ldx, out, ldo, C)) {
+  if ((RMS_COLS & 1) && cols_ok(x, ldx, out, ldo, C)) {
     hipLaunchKernelGGL(rms_rope_fwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
                        dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)x, ldx, (int)L, (int)C, w,
                        eps, (const float2*)rope_tab, (int)F, (int)Hg, (int)Wg, row0, (bf16*)out, ldo,
@@ -1091,7 +1092,7 @@ extern "C" int prfl_rms_rope_bwd_pos(const void* dout, int64_t lddo, const void*
   if (bad_c(C) || row0 < 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   prfl_prof::begin(KID_RMS, s);
-  if (RMS_COLS && cols_ok(x, ldx, dx, lddx, C) && cols_ok(dout, lddo, dout, lddo, C)) {
+  if ((RMS_COLS & 2) && cols_ok(x, ldx, dx, lddx, C) && cols_ok(dout, lddo, dout, lddo, C)) {
     static_assert(RC_ROWS == BWD_ROWS, "one partial row per prfl_norm_rows_per_part rows");
     hipLaunchKernelGGL(rms_rope_bwd_cols_kernel, dim3((L + RC_ROWS - 1) / RC_ROWS),
                        dim3(((C / 16) + 63) / 64 * 64), 0, s, (const bf16*)dout, lddo, (const bf16*)x,

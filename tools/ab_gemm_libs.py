@@ -52,12 +52,14 @@ def main():
 
         def call(lib, o, pas):
             if pas.endswith("_t"):    # forward passes on the transposed weight (MN-major B)
-                epi = {"fwd_t": 0, "gelu_t": 1, "resid_t": 2}[pas]
+                # residna_t: the gated residual without the saved y (the no-grad rollout's form)
+                epi = {"fwd_t": 0, "gelu_t": 1, "resid_t": 2, "residna_t": 2}[pas]
                 rc = lib.prfl_gemm_bf16_tiled(x.data_ptr(), K, 1, wt.data_ptr(), N, 0, o.data_ptr(), N, L, N, K,
                                               epi, bias.data_ptr() if a.bias else None,
                                               gate.data_ptr() if epi == 2 else None,
                                               res.data_ptr() if epi == 2 else None, N, 0,
-                                              aux.data_ptr() if epi else None, N, 0, tile_of[id(lib)], st)
+                                              aux.data_ptr() if epi and pas != "residna_t" else None, N, 0,
+                                              tile_of[id(lib)], st)
                 assert rc == 0, rc
                 return
             if pas == "fwd":   # y[L,N] = x[L,K] w[N,K]^T
@@ -104,6 +106,7 @@ def main():
             o["fwd_t"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
             o["gelu_t"] = torch.empty(L, N, device=dev, dtype=torch.bfloat16)
             o["resid_t"] = torch.empty(L, N, device=dev)
+            o["residna_t"] = torch.empty(L, N, device=dev)
         for pas in a.passes.split(","):
             ts = [[] for _ in libs]
             for r in range(a.reps + 1):
