@@ -478,6 +478,14 @@ def test_flash_attention_api():
     for b, kl in enumerate([90, 41]):
         ref = O.attention(q[b:b + 1], k[b:b + 1], v[b:b + 1], k_len=kl if kl < 90 else None)
         assert rel(out[b:b + 1], ref) < 5e-3
+    # full q_lens (the only lengths the reference's unflatten accepts) change nothing; k_lens as
+    # a device tensor or a list give the same result; q_scale multiplies the bf16 q (attention.py:86)
+    out2 = flash_attention(q.to(DEV), k.to(DEV), v.to(DEV), q_lens=torch.tensor([70, 70], device=DEV),
+                           k_lens=torch.tensor([90, 41], device=DEV))
+    assert torch.equal(out2, out)
+    out3 = flash_attention(q.to(DEV), k.to(DEV), v.to(DEV), k_lens=[90, 41], q_scale=0.5)
+    ref3 = flash_attention(q.to(DEV).to(torch.bfloat16) * 0.5, k.to(DEV), v.to(DEV), k_lens=[90, 41])
+    assert torch.equal(out3, ref3.float())
 
 
 def test_toy_pavrm_steps_vs_reference(golden):

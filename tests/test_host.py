@@ -347,3 +347,22 @@ def test_sp_state_follows_reference_parallel_states(monkeypatch, state):
         assert sp.current() is None
     finally:
         sp.clear()
+
+
+def test_flash_attention_length_arguments():
+    """`q_lens` / `k_lens` host logic of the drop-in (wan/modules/attention.py:63-80, 110): full
+    q_lens are accepted, shorter ones fail as the reference's unflatten does, bad k_lens are
+    refused before any device work (the checks run ahead of the custom op, so no GPU here)."""
+    from prfl_amd import attention as A
+    q = torch.zeros(2, 6, 1, 128)
+    k = torch.zeros(2, 9, 1, 128)
+    with pytest.raises(RuntimeError, match="unflattened"):
+        A.flash_attention(q, k, k, q_lens=torch.tensor([6, 4]))
+    with pytest.raises(ValueError, match="entries"):
+        A.flash_attention(q, k, k, k_lens=[9])
+    with pytest.raises(ValueError, match="outside"):
+        A.flash_attention(q, k, k, k_lens=torch.tensor([9, 10]))
+    with pytest.raises(ValueError, match="outside"):
+        A.flash_attention(q, k, k, k_lens=[0, 9])
+    assert A._lens(torch.tensor([6, 6], dtype=torch.int32), 2, 6, "q_lens") == [6, 6]
+    assert A._lens((3, 9), 2, 9, "k_lens", lo=1) == [3, 9]
