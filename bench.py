@@ -184,7 +184,7 @@ def cores_per_socket():
     return None
 
 
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_attn_fwd720_final.txt")
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06_pmc_attn720.txt")
 
 
 def pmc_traffic(L):
