@@ -527,6 +527,16 @@ def main():
                                       (1e9 if k in ("ln", "rms", "eltwise", "adamw") else 1e12), 1)}
                     for k, v in prof.items() if v["count"]},
     }
+    bw = [prof[k] for k in ("attn_bwd_dkdv", "attn_bwd_dq") if k in prof and prof[k]["count"]]
+    if len(bw) == 2:
+        # the two backward kernels are credited 8 + 6 = 14 L^2 d H (each recomputes S and dP);
+        # the algorithmic backward is 8 (dV, dP, dQ, dK), FA2's with one S recompute 10
+        w14, t_bw = sum(v["work"] for v in bw), sum(v["ms"] for v in bw) * 1e-3
+        res["attn_bwd"] = {"ms": round(t_bw * 1e3, 1),
+                           "credited_tflops": round(w14 / t_bw / 1e12, 1),
+                           "fa2_tflops": round(w14 * 10 / 14 / t_bw / 1e12, 1),
+                           "algorithmic_tflops": round(w14 * 8 / 14 / t_bw / 1e12, 1),
+                           "units": "credited 14, FA2 10, algorithmic 8 x L^2 x d x H per backward"}
     if tail_ms:
         res["grad_allreduce_exposed_tail_ms"] = {
             "per_backward": [round(t, 2) for t in tail_ms], "backend": args.dist_backend,
