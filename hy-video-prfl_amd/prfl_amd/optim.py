@@ -60,6 +60,7 @@ class AdamW:
         self.state_on_host = state_on_host
         self.overlap = overlap
         self.ring_slots = ring_slots
+        self.duplex = True          # D2H on its own copy stream (False: both directions on one)
         self._ring = None
         self._streams = None
         self._ready = {}            # param -> event (optimizer stream) after its final write
@@ -259,8 +260,8 @@ class AdamW:
             dev = live[0].device
             main = torch.cuda.current_stream(dev)
             if self._streams is None:
-                self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
-            opt, cp = self._streams
+                self._streams = tuple(torch.cuda.Stream(device=dev) for _ in range(3))
+            opt, cp, dn = self._streams
             self.wait(live)                         # a previous step still in flight
             opt.wait_stream(main)                   # grads (clipped) and params are final
         host = self._host_params()
@@ -289,7 +290,7 @@ class AdamW:
                 # start on `cp` at once, beside the device updates
                 done = self._update_device([u for u in units if u[0] not in host], lr, zero_grad)
                 done.update(self._update_streamed([u for u in units if u[0] in host], lr, opt, cp,
-                                                  zero_grad))
+                                                  dn if self.duplex else cp, zero_grad))
                 if self.shard:
                     for p in glive:
                         if p in done:
@@ -344,10 +345,12 @@ class AdamW:
             done[p] = ev
         return done
 
-    def _update_streamed(self, units, lr, opt, cp, zero_grad=False):
-        """Moments host -> ring -> kernel -> host, one copy stream for both directions: copy
-        stream order H2D(0..k-1), then per tensor i: D2H(i) after kernel(i), H2D(i+k) into the
-        slot D2H(i) just drained."""
+    def _update_streamed(self, units, lr, opt, cp, dn, zero_grad=False):
+        """Moments host -> ring -> kernel -> host with the two directions on two copy streams, so
+        PCIe carries both at once (full duplex): `cp` H2D(0..k-1), then H2D(i+k) into the slot
+        once D2H(i) on `dn` has drained it; `dn` D2H(i) after kernel(i) on `opt`.  (One stream for
+        both directions ran them in turn: the last update of a run, which nothing hides, moved
+        its moments at one direction's rate.)"""
         done = {}
         if not units:
             return done
@@ -358,9 +361,13 @@ class AdamW:
             self._ring = [torch.empty(2 * nmax, dtype=torch.float32, device=dev) for _ in range(k)]
             for buf in self._ring:
                 buf.record_stream(cp)
+                buf.record_stream(dn)
         cap = self._ring[0].numel() // 2
         slots = [(buf[:cap], buf[cap:2 * cap]) for buf in self._ring]
-        h2d_ev = [None] * len(units)
+        h2d_ev, d2h_ev = [None] * len(units), [None] * len(units)
+        # the ring and the host moments are reused across steps and groups: every earlier D2H
+        # (slot drained, host copy written) precedes this call's first H2D
+        cp.wait_stream(dn)
 
         def h2d(i):
             p, a, b = units[i]
@@ -368,12 +375,13 @@ class AdamW:
             m_d, v_d = slots[i % k]
             n = b - a
             with torch.cuda.stream(cp):
+                if i >= k:
+                    cp.wait_event(d2h_ev[i - k])
                 m_d[:n].copy_(m_h, non_blocking=True)
                 v_d[:n].copy_(v_h, non_blocking=True)
                 h2d_ev[i] = torch.cuda.Event()
                 h2d_ev[i].record(cp)
 
-        # the ring is reused across steps and groups: earlier D2H copies are earlier on `cp`
         for i in range(min(k, len(units))):
             h2d(i)
         for i, (p, a, b) in enumerate(units):
@@ -390,10 +398,12 @@ class AdamW:
             ev.record(opt)
             done[p] = ev
             m_h, v_h = self._state(p)
-            with torch.cuda.stream(cp):
-                cp.wait_event(ev)
+            with torch.cuda.stream(dn):
+                dn.wait_event(ev)
                 m_h.copy_(m_d[:n], non_blocking=True)
                 v_h.copy_(v_d[:n], non_blocking=True)
+                d2h_ev[i] = torch.cuda.Event()
+                d2h_ev[i].record(dn)
             if i + k < len(units):
                 h2d(i + k)
         return done
