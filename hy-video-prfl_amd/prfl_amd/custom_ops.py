@@ -46,8 +46,9 @@ def _meta(num_heads, grid, seq_lens, rope_tab, i2v, eps, fp8, sp=0):
 def wan_block(x: Tensor, e: Tensor, context: Tensor, params: List[Tensor], num_heads: int,
               grid: List[int], seq_lens: List[int], rope_tab: Tensor, i2v: bool, eps: float,
               fp8: int, keep_attn: bool, sp: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
-    """fp8: 0 bf16, 1 e4m3 forward projections, 2 also the e4m3 self-attention forward
-    (config C5, block.Meta).  x [B, L, C] (fp32, or bf16 for block 0), e [B, 6, C] fp32 (modulation + e0), context
+    """fp8: block.fp8_code -- bits 0-1 0 bf16, 1 e4m3 forward projections, 2 also the e4m3
+    self-attention forward (config C5, block.Meta), from bit 2 the projections kept bf16; sp: 0
+    or the prfl_amd.sp handle of the sequence-parallel group (Ulysses, block.Meta.sp).  x [B, L, C] (fp32, or bf16 for block 0), e [B, 6, C] fp32 (modulation + e0), context
     [B, Lc, C] bf16, params in block.param_names(i2v) order, grid = flattened (F, H, W) per
     sample.  Returns (out fp32 [B, L, C], kept self-attention output bf16 [B, L, C] and LSE fp32
     [B, H, L] when keep_attn, else empty).  sp: a sequence-parallel group handle (prfl_amd.sp;
