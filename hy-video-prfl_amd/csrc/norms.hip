@@ -257,7 +257,16 @@ __global__ __launch_bounds__(NT) void rms_rope_bwd_kernel(
 #ifndef RMS_WAVE
 #define RMS_WAVE 1
 #endif
-constexpr int RW_RPW = 4;     // rows per wave in the forward (16 rows per workgroup)
+#ifndef RMS_WAVE_RPW
+#define RMS_WAVE_RPW 4
+#endif
+// forward row prefetch: 0 none (one row in flight per wave, 90 VGPRs), 1 the next row into a
+// second register set (unrolled), 2 the same in a rolled loop, the prefetched set copied into the
+// working one; 720p 0.337 / 0.332 / 0.313 ms, bit-identical (profiles/r06_ab_rms_prefetch.txt)
+#ifndef RMS_WAVE_PF
+#define RMS_WAVE_PF 2
+#endif
+constexpr int RW_RPW = RMS_WAVE_RPW;     // rows per wave in the forward (16 rows per workgroup)
 constexpr int RW_NJ = 10;     // 16-B chunks per lane: C <= 64 * 10 * 8 = 5120
 
 __device__ __forceinline__ void rope_cs4(const float2* __restrict__ tab, int pair0, int pf, int ph,
@@ -271,22 +280,49 @@ __global__ __launch_bounds__(NT) void rms_rope_fwd_wave_kernel(
     const float2* __restrict__ tab, int F, int Hg, int Wg, int64_t row0, bf16* __restrict__ out,
     int64_t ldo, float* __restrict__ rstd_out, float oscale) {
   __shared__ f32x4 ws[RW_NJ * 64 * 2];
-  for (int c = threadIdx.x; c < C / 4; c += NT) ws[c] = ldf4(w, c * 4);
-  __syncthreads();
   const int lane = threadIdx.x & 63, nc = C / 8, pair0 = ((lane * 8) & 127) >> 1;
   const int64_t rbase = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RW_RPW;
+  // RMS_WAVE_PF: the next row's chunks are loaded before this row's normalise / store, and the
+  // first row's before the w staging and its barrier
+  bf16x8 v[2][RW_NJ];
+  auto load = [&](int64_t row, bf16x8 (&d)[RW_NJ]) {
+#pragma unroll
+    for (int j = 0; j < RW_NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc && row < L) d[j] = *(const bf16x8*)(x + row * ldx + c * 8);
+    }
+  };
+  if (RMS_WAVE_PF) load(rbase, v[0]);
+  for (int c = threadIdx.x; c < C / 4; c += NT) ws[c] = ldf4(w, c * 4);
+  __syncthreads();
+#if RMS_WAVE_PF == 2
+#pragma unroll 1
+#else
+#pragma unroll
+#endif
   for (int rr = 0; rr < RW_RPW; ++rr) {
     const int64_t row = rbase + rr;
     if (row >= L) return;
-    bf16x8 v[RW_NJ];
+    // PF 2: rolled loop, the prefetched set copied into the working one (fewer live registers)
+    bf16x8 (&cur)[RW_NJ] = v[RMS_WAVE_PF == 1 ? (rr & 1) : 0];
+    if (!RMS_WAVE_PF) {
+      load(row, cur);
+    } else if (RMS_WAVE_PF == 2) {
+      if (rr > 0) {
+#pragma unroll
+        for (int j = 0; j < RW_NJ; ++j) cur[j] = v[1][j];
+      }
+      if (rr + 1 < RW_RPW) load(row + 1, v[1]);
+    } else if (rr + 1 < RW_RPW) {
+      load(row + 1, v[(rr + 1) & 1]);
+    }
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < RW_NJ; ++j) {
       const int c = lane + 64 * j;
       if (c < nc) {
-        v[j] = *(const bf16x8*)(x + row * ldx + c * 8);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) ss += bf2f(v[j][r]) * bf2f(v[j][r]);
+        for (int r = 0; r < 8; ++r) ss += bf2f(cur[j][r]) * bf2f(cur[j][r]);
       }
     }
     const float rstd = rsqrtf(wave_sum(ss) / C + eps);
@@ -304,8 +340,8 @@ __global__ __launch_bounds__(NT) void rms_rope_fwd_wave_kernel(
         float y[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          y[r] = mul_rn(bfr(bf2f(v[j][r]) * rstd), w0[r]);
-          y[r + 4] = mul_rn(bfr(bf2f(v[j][r + 4]) * rstd), w1[r]);
+          y[r] = mul_rn(bfr(bf2f(cur[j][r]) * rstd), w0[r]);
+          y[r + 4] = mul_rn(bfr(bf2f(cur[j][r + 4]) * rstd), w1[r]);
         }
         bf16x8 o;
         if (rot) {
@@ -676,6 +712,8 @@ __global__ __launch_bounds__(RC_MAXT) void rms_rope_bwd_cols_kernel(
 #ifndef LN_RPW
 #define LN_RPW 4
 #endif
+// (the next row prefetched into a second register set, as RMS_WAVE_PF 2: 0.448 vs 0.449 ms at
+// 720p, profiles/r06_ab_rms_prefetch.txt -- not kept)
 constexpr int RPW = LN_RPW;   // rows per wave -> 16 rows per workgroup
 __global__ __launch_bounds__(NT) void ln_mod_fwd_lds_kernel(
     const void* __restrict__ x, int x_bf16, int64_t ldx, int L, int C,
