@@ -16,7 +16,6 @@
 //   attn_delta_kernel     D = rowsum(dO * O) (FA2)
 //   attn_bwd_dkdv_kernel  dK, dV: 8 waves x 32 keys, Q/dO tiles streamed, no atomics
 //   attn_bwd_dq_kernel    dQ: 8 waves x 32 queries, 96-key K/V tiles streamed
-#include <type_traits>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -1234,249 +1233,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   bp.flush(0, w, lane);
 #endif
   if (part) {            // unscaled partial dK^T / dV^T of this query share (attn_merge_kv)
-    const int64_t r = (int64_t)(blockIdx.x - a.nmain_k) * 256 + w * 32 + l32;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int c = dt * 32 + 8 * rg + 4 * hh;
-        *(f32x4*)(a.Pk + r * HD + c) =
-            (f32x4){dk[dt][rg * 4], dk[dt][rg * 4 + 1], dk[dt][rg * 4 + 2], dk[dt][rg * 4 + 3]};
-        *(f32x4*)(a.Pv + r * HD + c) =
-            (f32x4){dv[dt][rg * 4], dv[dt][rg * 4 + 1], dv[dt][rg * 4 + 2], dv[dt][rg * 4 + 3]};
-      }
-  } else if (key < a.Lk) {
-    bf16* dKb = a.dK + b * a.bdk + h * HD + (int64_t)key * a.lddk;
-    bf16* dVb = a.dV + b * a.bdv + h * HD + (int64_t)key * a.lddv;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        bf16x4 vk, vv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          vk[r] = f2bf(kvalid ? dk[dt][rg * 4 + r] * a.scale : 0.f);
-          vv[r] = f2bf(kvalid ? dv[dt][rg * 4 + r] : 0.f);
-        }
-        *(bf16x4*)(dKb + dt * 32 + 8 * rg + 4 * hh) = vk;
-        *(bf16x4*)(dVb + dt * 32 + 8 * rg + 4 * hh) = vv;
-      }
-  }
-}
-
-// dK/dV with the two halves of the workgroup skewed by half a sub-tile (round 6; VERDICT r05 #2,
-// profiles/r06_attn_bwd_phases.txt): in attn_bwd_dkdv_kernel both waves of a SIMD run the same
-// phase at the same time (one barrier per tile), so the softmax / pack / DMA-issue VALU of one
-// finds no MFMAs of the other to hide behind, and the older half parks 16-18 % at the barrier.
-// Here the tile is one 32-query sub-tile and waves 0-3 ("lead") run [S / dP chain, softmax, dV /
-// dK chain] of sub-tile i between barriers i-1 and i, while waves 4-7 ("lag") run [softmax, dV /
-// dK chain] of sub-tile i-1 (its S / dP accumulators held across the barrier -- the same registers
-// as inside a sub-tile) and then the S / dP chain of sub-tile i: after every barrier one wave of
-// each SIMD multiplies while the other exponentiates.  The lag reads sub-tile i-1's stage while
-// sub-tile i+1 lands, so the ring holds three 32-query stages (3 x 16.5 KiB beside the 64 KiB V
-// image).  Same per-element arithmetic and accumulation order as attn_bwd_dkdv_kernel:
-// bit-identical outputs.
-#ifndef ATTN_DKDV_SKEW
-#define ATTN_DKDV_SKEW 0
-#endif
-template <bool QS>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_skew_kernel(AttnBwdArgs a) {
-  // the ring first: every stage offset fits a ds_read immediate (the main loop is unrolled by
-  // three so each stage is a constant); V after it, its addresses per-lane VGPRs anyway
-  constexpr int V_BYTES = 256 * 256, STAGE = 8192 * 2 + 512, NS = 3;
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + V_BYTES];
-  int unit, share;
-  bool part;
-  tail_unit(a.nmain_k, a.split_k, unit, share, part);
-  const int nkt = (a.Lk + 255) / 256;
-  int b, h, kt0;
-  bwd_unit<ATTN_BWD_XCD_KV>(unit, nkt, a.H, a.B, b, h, kt0);
-  const int k0 = kt0 * 256;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (ATTN_BWD_PRIO & 1 && w >= 4) __builtin_amdgcn_s_setprio(1);
-  const bool lead = w < 4;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  const bf16* Qb = a.Q + b * a.bq + h * HD;
-  const bf16* Kb = a.K + b * a.bk + h * HD;
-  const bf16* Vb = a.V + b * a.bv + h * HD;
-  const bf16* dOb = a.dO + b * a.bdo + h * HD;
-  const float* lseb = a.LSE + ((int64_t)b * a.H + h) * a.Lq;
-  const float* delb = a.Delta + ((int64_t)b * a.H + h) * a.Lq;
-  const int key = k0 + w * 32 + l32;
-  const bool kvalid = key < a.k_len;
-  const int kr = min(key, a.Lk - 1);
-  bf16x8 kf[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) kf[ks] = *(const bf16x8*)(Kb + (int64_t)kr * a.ldk + ks * 16 + hh * 8);
-  if (QS) {
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) kf[ks] = -kf[ks];
-  }
-  char* Vs = smem + NS * STAGE;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int piece = w * 8 + i, row = piece * 4 + (lane >> 4), pc = lane & 15;
-    const int kk = min(k0 + row, a.Lk - 1);
-    dma16(Vb + (int64_t)kk * a.ldv + ((pc ^ (row & 15)) << 3), lds_addr(Vs + piece * 1024));
-  }
-  // one Q and one dO piece (4 rows) per wave per sub-tile, offB image; LSE / D rows by waves 0 / 1
-  uint32_t voq, vod;
-  {
-    const int row = w * 4 + (lane >> 4), pc = lane & 15;
-    const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-    voq = (uint32_t)(row * a.ldq * 2) + ((pc ^ swzb) << 4);
-    vod = (uint32_t)(row * a.lddo * 2) + ((pc ^ swzb) << 4);
-  }
-  // the workgroup's 64-query tiles [t0, t0 + nq) (the split of attn_bwd_dkdv_kernel), as ns
-  // sub-tiles of 32 from query s0 * 32
-  int t0 = 0, nq = (a.Lq + 63) / 64;
-  if (part) {
-    const int per = (nq + a.split_k - 1) / a.split_k;
-    t0 = min(share * per, nq);
-    nq = min(nq, t0 + per) - t0;
-  }
-  const int s0 = t0 * 2;
-  const int ns = nq > 0 ? (min(a.Lq, (t0 + nq) * 64) - t0 * 64 + 31) / 32 : 0;
-  auto dma_sub = [&](int j, int st) __attribute__((always_inline)) {
-    char* Qs = smem + st * STAGE;
-    const int qb = (s0 + j) * 32, rows = min(a.Lq - qb, 32);
-    dma16_buf(make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2)), voq, 0,
-              lds_addr(Qs + w * 1024));
-    dma16_buf(make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2)), vod, 0,
-              lds_addr(Qs + 8192 + w * 1024));
-    if (w < 2) {
-      uint32_t l4;
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
-                   "v_lshlrev_b32 %0, 2, %0" : "=v"(l4));
-      dma4_buf(make_srd((w == 0 ? lseb : delb) + qb, (uint32_t)(rows * 4)), l4,
-               lds_addr(Qs + 16384 + w * 256));
-    }
-  };
-  f32x16 dk[4], dv[4], sacc, dpt;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
-  // S = Q.K^T (from +LSE under QS) and dP = dO.V^T (from -D under NEGD) of sub-tile j
-  auto chain1 = [&](auto S) __attribute__((always_inline)) {
-    const char* Qs = smem + decltype(S)::value * STAGE;
-    const char* Ds = Qs + 8192;
-    const float* Ls = (const float*)(Qs + 16384);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpt[r] = 0.f; }
-    if (ATTN_BWD_NEGD) {
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const f32x4 d4 = *(const f32x4*)(Ls + 64 + 8 * rg + 4 * hh);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dpt[rg * 4 + r] = d4[r];
-      }
-    }
-    if (QS) {
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const f32x4 l4 = *(const f32x4*)(Ls + 8 * rg + 4 * hh);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sacc[rg * 4 + r] = l4[r];
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      sacc = mfma32(*(const bf16x8*)(Qs + offB(l32, (ks * 2 + hh) * 16)), kf[ks], sacc);
-      const bf16x8 vfr = *(const bf16x8*)(Vs + off16(w * 32 + l32, ks * 2 + hh));
-      dpt = mfma32(*(const bf16x8*)(Ds + offB(l32, (ks * 2 + hh) * 16)), vfr, dpt);
-      if (ks & 1 & ATTN_DKDV_SB) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // P, dS of sub-tile j from its accumulators, then dV^T += dO^T P, dK^T += Q^T dS; the next
-  // sub-tile's pieces are issued after the softmax (dma >= 0, into stage dst)
-  auto finish = [&](int j, auto S, int dma, int dst) __attribute__((always_inline)) {
-    const char* Qs = smem + decltype(S)::value * STAGE;
-    const char* Ds = Qs + 8192;
-    const float* Ls = (const float*)(Qs + 16384);
-    const int qb = (s0 + j) * 32;
-    const bool tail = qb + 32 > a.Lq;
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const int q4 = 8 * rg + 4 * hh;
-      const f32x4 l4 = *(const f32x4*)(Ls + q4);
-      const f32x4 d4 = *(const f32x4*)(Ls + 64 + q4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = QS ? __builtin_amdgcn_exp2f(-sacc[rg * 4 + r])
-                           : __builtin_amdgcn_exp2f(sacc[rg * 4 + r] * a.sl2 - l4[r]);
-        sacc[rg * 4 + r] = p;
-        dpt[rg * 4 + r] = ATTN_BWD_NEGD ? p * dpt[rg * 4 + r] : p * (dpt[rg * 4 + r] - d4[r]);
-      }
-      if (__builtin_expect(tail, 0)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (qb + q4 + r >= a.Lq) { sacc[rg * 4 + r] = 0.f; dpt[rg * 4 + r] = 0.f; }
-      }
-    }
-    if (dma >= 0) dma_sub(dma, dst);
-    bf16x8 pk[2], dk8[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      pk[s2] = (bf16x8){f2bf(sacc[8 * s2 + 0]), f2bf(sacc[8 * s2 + 1]), f2bf(sacc[8 * s2 + 2]),
-                        f2bf(sacc[8 * s2 + 3]), f2bf(sacc[8 * s2 + 4]), f2bf(sacc[8 * s2 + 5]),
-                        f2bf(sacc[8 * s2 + 6]), f2bf(sacc[8 * s2 + 7])};
-      dk8[s2] = (bf16x8){f2bf(dpt[8 * s2 + 0]), f2bf(dpt[8 * s2 + 1]), f2bf(dpt[8 * s2 + 2]),
-                         f2bf(dpt[8 * s2 + 3]), f2bf(dpt[8 * s2 + 4]), f2bf(dpt[8 * s2 + 5]),
-                         f2bf(dpt[8 * s2 + 6]), f2bf(dpt[8 * s2 + 7])};
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int byte = (dt * 32 + 16 * (g & 1) + 4 * pp) * 2;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int ra = 16 * s2 + 4 * (g >> 1) + qq;
-        const bf16x8 dof = cat8(lds_read_tr(Ds + offB(ra, byte)), lds_read_tr(Ds + offB(ra + 8, byte)));
-        const bf16x8 qtf = cat8(lds_read_tr(Qs + offB(ra, byte)), lds_read_tr(Qs + offB(ra + 8, byte)));
-        dv[dt] = mfma32(dof, pk[s2], dv[dt]);
-        dk[dt] = mfma32(qtf, dk8[s2], dk[dt]);
-      }
-      if (ATTN_DKDV_SB & 2) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // One code path for both halves, the barrier placed differently: lead = [S / dP chain j,
-  // finish j, barrier], lag = [S / dP chain j, barrier, finish j], so between barriers j-1 and j
-  // the lead runs chain j + finish j while the lag runs finish j-1 + chain j.  Sub-tile j+1's
-  // pieces must land before barrier j: the lead issues its pieces in finish j, the lag in
-  // finish j-1 (its stage last held sub-tile j-2, read before barrier j-1 by both halves).
-  // (each half's barrier: a uniform skip inside one asm block, s_waitcnt vmcnt(0) + s_barrier)
-  auto sync0 = [&]() __attribute__((always_inline)) {   // the lag's barrier (w >= 4)
-    asm volatile("s_cmp_lt_u32 %0, 4\n\ts_cbranch_scc1 1f\n\ts_waitcnt vmcnt(0)\n\ts_barrier\n1:"
-                 :: "s"(__builtin_amdgcn_readfirstlane(w)) : "memory", "scc");
-  };
-  auto sync1 = [&]() __attribute__((always_inline)) {   // the lead's barrier (w < 4)
-    asm volatile("s_cmp_lt_u32 %0, 4\n\ts_cbranch_scc0 1f\n\ts_waitcnt vmcnt(0)\n\ts_barrier\n1:"
-                 :: "s"(__builtin_amdgcn_readfirstlane(w)) : "memory", "scc");
-  };
-  auto step = [&](int j, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    using Cur = std::integral_constant<int, u>;
-    chain1(Cur{});
-    sync0();
-    const int nd = lead ? j + 1 : j + 2;
-    finish(j, Cur{}, nd < ns ? nd : -1, lead ? (u + 1) % NS : (u + 2) % NS);
-    sync1();
-  };
-  if (ns > 0) dma_sub(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): K fragments, V, sub-tile 0
-  __syncthreads();
-  if (!lead && ns > 1) dma_sub(1, 1);
-  // (written with the guards inside: the same loop with `j < ns` and breaks spilled ~230 VGPRs)
-  for (int j = 0; j <= ns; j += NS) {
-    if (j < ns) step(j, std::integral_constant<int, 0>{});
-    if (j + 1 > ns) break;
-    if (j + 1 < ns) step(j + 1, std::integral_constant<int, 1>{});
-    if (j + 2 > ns) break;
-    if (j + 2 < ns) step(j + 2, std::integral_constant<int, 2>{});
-  }
-  if (part) {
     const int64_t r = (int64_t)(blockIdx.x - a.nmain_k) * 256 + w * 32 + l32;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -2726,10 +2482,7 @@ int attn_bwd_impl(const void* q, int64_t ldq, int64_t bq, const void* k, int64_t
                 vt_keys(Lk) * HD};
   prfl_prof::begin(KID_ATTN_BWD_DKDV, s);
   const dim3 gk((unsigned)(nmain_k + rk * split_k));
-  if (ATTN_DKDV_SKEW && !ATTN_PHASETIME) {
-    if (l2q) hipLaunchKernelGGL(attn_bwd_dkdv_skew_kernel<true>, gk, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL(attn_bwd_dkdv_skew_kernel<false>, gk, dim3(512), 0, s, a);
-  } else if (l2q) {
+  if (l2q) {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, gk, dim3(512), 0, s, a);
   } else {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, gk, dim3(512), 0, s, a);
