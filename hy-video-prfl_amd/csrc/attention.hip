@@ -339,9 +339,12 @@ __device__ __forceinline__ float xhalf_max(float x) {
 #endif
 // the wave's K (and V) pieces of a tile under ONE m0 write (consecutive KiB of LDS, piece i at
 // instruction offset i KiB, pre-subtracted from its per-lane source offset) instead of a save /
-// set / s_nop / restore of m0 around every piece
+// set / s_nop / restore of m0 around every piece.  Round 6, on the PVFIRST / speculative-P
+// kernel: 720p forward 82.58 -> 82.15 ms, twice in one process, bit-identical (on the round-4
+// kernel it had tied); the K pieces in the MFMA phase (KDMA_X) measured 6 % slower
+// (profiles/r06_ab_fwd_dma.txt)
 #ifndef ATTN_FWD_DMA_GROUPED
-#define ATTN_FWD_DMA_GROUPED 0
+#define ATTN_FWD_DMA_GROUPED 1
 #endif
 #ifndef ATTN_G0_DMA_Y
 #define ATTN_G0_DMA_Y 1
