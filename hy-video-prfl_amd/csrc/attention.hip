@@ -982,6 +982,12 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(AttnArgs a) {
 #ifndef ATTN_DKDV_DMA_SPLIT
 #define ATTN_DKDV_DMA_SPLIT 0
 #endif
+// the backward kernels' Q / dO (dK/dV) and K / V (dQ) pieces under one m0 write per wave and
+// operand, as the forward's ATTN_FWD_DMA_GROUPED (per-lane offsets pre-subtract the instruction
+// offset: ld >= 128 keeps them non-negative)
+#ifndef ATTN_BWD_DMA_GROUPED
+#define ATTN_BWD_DMA_GROUPED 1
+#endif
 // dK/dV scheduling fences: bit 0 = one every two k-steps of the S / dP chain, bit 1 = one per
 // dV / dK d-tile (3 = both); 0 / 1 / 2 / 3 tie within 0.3 % (profiles/r04_ab_dkdv_sb.txt)
 #ifndef ATTN_DKDV_SB
@@ -1099,13 +1105,29 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     const int qb = (t0 + t) * 64, rows = min(a.Lq - qb, 64);   // record range < 2^32 bytes
     if (which & 1) {
       const i32x4 sq = make_srd(Qb + (int64_t)qb * a.ldq, (uint32_t)(rows * a.ldq * 2));
+      if (ATTN_BWD_DMA_GROUPED) {
+        unsigned keep;
+        m0_set(lds_addr(Qs + w * 2 * 1024), keep);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) dma16_buf(sq, voq[i], 0, lds_addr(Qs + (w * 2 + i) * 1024));
+        for (int i = 0; i < 2; ++i) dma16_buf_m0(sq, voq[i] - i * 1024, 0, i);
+        m0_restore(keep);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma16_buf(sq, voq[i], 0, lds_addr(Qs + (w * 2 + i) * 1024));
+      }
     }
     if (which & 2) {
       const i32x4 sd = make_srd(dOb + (int64_t)qb * a.lddo, (uint32_t)(rows * a.lddo * 2));
+      if (ATTN_BWD_DMA_GROUPED) {
+        unsigned keep;
+        m0_set(lds_addr(Ds + w * 2 * 1024), keep);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) dma16_buf(sd, vod[i], 0, lds_addr(Ds + (w * 2 + i) * 1024));
+        for (int i = 0; i < 2; ++i) dma16_buf_m0(sd, vod[i] - i * 1024, 0, i);
+        m0_restore(keep);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma16_buf(sd, vod[i], 0, lds_addr(Ds + (w * 2 + i) * 1024));
+      }
     }
     if ((which & 1) && w < 2) {   // lane * 4 re-derived here (volatile: not hoisted into a register kept live)
       uint32_t l4;
@@ -1354,16 +1376,35 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     const i32x4 sv = make_srd(Vb + (int64_t)t * TK * a.ldv, (uint32_t)(rows * a.ldv * 2));
     uint32_t ln;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-#pragma unroll
-    for (int i = 0; i < NKT; ++i) {
+    auto offk = [&](int i) {
       const int row = (w * NKT + i) * 4 + (ln >> 4), pc = ln & 15;
       const int swzb = ((row & 3) << 2) | ((row >> 2) & 3);
-      if (which & 1)
-        dma16_buf(sk, (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4), 0,
-                  lds_addr(Ks + (w * NKT + i) * 1024));
-      if (which & 2)
-        dma16_buf(sv, (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4), 0,
-                  lds_addr(Vs + (w * NKT + i) * 1024));
+      return (uint32_t)(row * a.ldk * 2) + ((pc ^ swzb) << 4);
+    };
+    auto offv = [&](int i) {
+      const int row = (w * NKT + i) * 4 + (ln >> 4), pc = ln & 15;
+      return (uint32_t)(row * a.ldv * 2) + ((pc ^ (row & 15)) << 4);
+    };
+    if (ATTN_BWD_DMA_GROUPED && NKT <= 4) {   // one m0 per operand (see the forward's DMAG)
+      unsigned keep;
+      if (which & 1) {
+        m0_set(lds_addr(Ks + w * NKT * 1024), keep);
+#pragma unroll
+        for (int i = 0; i < NKT; ++i) dma16_buf_m0(sk, offk(i) - i * 1024, 0, i);
+        m0_restore(keep);
+      }
+      if (which & 2) {
+        m0_set(lds_addr(Vs + w * NKT * 1024), keep);
+#pragma unroll
+        for (int i = 0; i < NKT; ++i) dma16_buf_m0(sv, offv(i) - i * 1024, 0, i);
+        m0_restore(keep);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NKT; ++i) {
+        if (which & 1) dma16_buf(sk, offk(i), 0, lds_addr(Ks + (w * NKT + i) * 1024));
+        if (which & 2) dma16_buf(sv, offv(i), 0, lds_addr(Vs + (w * NKT + i) * 1024));
+      }
     }
     if (KT) {          // K^T tile: one contiguous 24 KiB run, lane-linear pieces
       const i32x4 skt = make_srd(KTb + (int64_t)t * TK * HD, (uint32_t)SV);
